@@ -1,0 +1,252 @@
+"""Benchmark: rasterize fwd+bwd Mpixels/s at 256^2, batch 64 per GPU (BASELINE.json metric).
+
+Workload (synthetic, no files): ico-sphere level 4 (V=2562, F=5120), per-item
+vertex jitter and viewpoint, projected once outside the timed region; shared 4x4-per-face texture
+atlas (create_textures, 3x288x288, U(0,1)) expanded over the batch; RasterizeHyperparam defaults
+(anti-aliasing on -> 512^2 internal, draw_backside, rgb + silhouettes + depth -> C = 5).
+One step = rasterize_core forward + backward with a fixed N(0,1) upstream gradient (the gradient
+of (images * G).sum()), producing d/dvertices and d/dtextures.
+
+Multi-GPU: one process per GPU (torchrun), each renders its own 64 items (batch sharding, weak
+scaling, no collective on the data path); the timed region is bracketed by barriers and the max
+over ranks is reported.  With --gather the rank images are also all-gathered over RCCL after the
+timed region and that time is reported separately.
+
+Output: one JSON line on rank 0 (see README/DESIGN for field meanings).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=64, help="items per GPU")
+    p.add_argument("--image-size", type=int, default=256)
+    p.add_argument("--level", type=int, default=4, help="ico-sphere subdivision level (4 -> 5120 faces)")
+    p.add_argument("--mode", choices=["rgbsd", "sil"], default="rgbsd")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--gather", action="store_true", help="also time an RCCL all_gather of the images")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.device("cuda", local if world > 1 else 0)
+
+
+def workload(args, rank, dev):
+    import neural_renderer_v2_pytorch_amd as nr
+    from neural_renderer_v2_pytorch_amd import synthetic
+    B = args.batch
+    v, f = synthetic.icosphere(args.level)
+    items = np.arange(rank * B, (rank + 1) * B)
+    vb = np.stack([synthetic.jittered(v, 1, seed_base=1000 + int(i))[0] for i in items])
+    eyes = np.stack([synthetic.viewpoints(1, seed_base=2000 + int(i))[0] for i in items])
+    proj = synthetic.project(torch.as_tensor(vb, device=dev), torch.as_tensor(eyes, device=dev)).contiguous()
+    proj = proj.detach().requires_grad_(True)
+    faces = torch.as_tensor(f, device=dev)
+    hp = nr.RasterizeHyperparam(image_size=args.image_size)
+    if args.mode == "rgbsd":
+        vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+        tex = np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32)
+        tex = torch.as_tensor(tex, device=dev).requires_grad_(True)
+        params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                                   faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+        C = 5
+    else:
+        params, tex, C = nr.RasterizeParam(), None, 1
+        hp.draw_rgb, hp.draw_depth = False, False
+    g = torch.as_tensor(np.random.RandomState(7).normal(size=(B, C, args.image_size, args.image_size))
+                        .astype(np.float32), device=dev)
+    return dict(nr=nr, proj=proj, faces=faces, params=params, hp=hp, tex=tex, g=g, C=C, V=v.shape[0],
+                F=f.shape[0], tex_shape=None if tex is None else tuple(tex.shape))
+
+
+def step(w):
+    from neural_renderer_v2_pytorch_amd.rasterize import rasterize_core
+    w["proj"].grad = None
+    if w["tex"] is not None:
+        w["tex"].grad = None
+    images = rasterize_core(w["proj"], w["faces"], w["params"], w["hp"])
+    images.backward(w["g"])
+    return images
+
+
+def kernel_bytes(w, args):
+    """Algorithmic (compulsory) bytes per launch of each kernel, SURVEY.md section 8d / DESIGN.md."""
+    B, s, C, V, F = args.batch, args.image_size, w["C"], w["V"], w["F"]
+    S = 2 * s
+    T = 0 if w["tex_shape"] is None else 3 * w["tex_shape"][1] * w["tex_shape"][2] * 4
+    fwd = 4 * S * S * B + 4 * C * s * s * B + 36 * F * B + T
+    bwd = 4 * S * S * B + 4 * C * s * s * B + 36 * F * B + 12 * V * B + 2 * T
+    setup = 12 * V * B + 12 * F + 36 * F * B + 8 * F * B
+    total = B * (8 * S * S + 8 * C * s * s + 36 * V) + 24 * F + (2 * T if T else 0)
+    return dict(fwd=fwd, bwd=bwd, setup=setup, total=total)
+
+
+def time_kernels(w, n=10):
+    """HIP-event timing of the library's forward and backward calls on the launch stream."""
+    from neural_renderer_v2_pytorch_amd.rasterize import rasterize_core
+    stream = torch.cuda.current_stream()
+    fwd_ms, bwd_ms = [], []
+    for _ in range(n):
+        w["proj"].grad = None
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record(stream)
+        images = rasterize_core(w["proj"], w["faces"], w["params"], w["hp"])
+        e1.record(stream)
+        images.backward(w["g"])
+        e2.record(stream)
+        torch.cuda.synchronize()
+        fwd_ms.append(e0.elapsed_time(e1))
+        bwd_ms.append(e1.elapsed_time(e2))
+    return float(np.median(fwd_ms)), float(np.median(bwd_ms))
+
+
+def cpu_baseline(args, budget_s):
+    """The CPU oracle (C brute-force kernels with OpenMP + torch CPU stages of rasterize_core), timed
+    on this host on whole items of the same workload until ~budget_s seconds have been spent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import neural_renderer_v2_pytorch_amd as nr
+    from neural_renderer_v2_pytorch_amd import synthetic
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    v, f = synthetic.icosphere(args.level)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.as_tensor(np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32)).requires_grad_(True)
+    C = 5 if args.mode == "rgbsd" else 1
+    oracle.lib()
+    done, t_total = 0, 0.0
+    while t_total < budget_s and done < args.batch:
+        vb = torch.as_tensor(synthetic.jittered(v, 1, seed_base=1000 + done))
+        eye = torch.as_tensor(synthetic.viewpoints(1, seed_base=2000 + done))
+        proj = synthetic.project(vb, eye).detach().requires_grad_(True)
+        g = torch.as_tensor(np.random.RandomState(7).normal(size=(1, C, args.image_size, args.image_size))
+                            .astype(np.float32))
+        t0 = time.perf_counter()
+        if args.mode == "rgbsd":
+            img = oracle.rasterize_core(proj, f, image_size=args.image_size, vertices_textures=torch.as_tensor(vt)[None],
+                                        faces_textures=ft, textures=tex[None])
+        else:
+            img = oracle.rasterize_core(proj, f, image_size=args.image_size, draw_rgb=False, draw_depth=False)
+        img.backward(g)
+        t_total += time.perf_counter() - t0
+        done += 1
+    mpx = done * args.image_size ** 2 / t_total / 1e6
+    return dict(value=mpx, unit="Mpixels/s", cores=threads, kind="port",
+                sample="%d item(s) of the headline workload (1 item = 256^2 output, 512^2 internal, %d faces, "
+                       "fwd+bwd), %.1f s; oracle/nr_oracle.c brute force (OpenMP) + torch-CPU stages"
+                       % (done, f.shape[0], t_total))
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    w = workload(args, rank, dev)
+    for _ in range(args.warmup):
+        step(w)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        images = step(w)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    px = world * args.batch * args.image_size ** 2 * args.steps
+    value = px / elapsed / 1e6
+
+    gather_ms = None
+    if args.gather and world > 1:
+        out = torch.empty((world,) + tuple(images.shape), device=dev, dtype=images.dtype)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        torch.distributed.all_gather_into_tensor(out, images.detach().contiguous())
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - t1) * 1e3
+
+    fwd_ms, bwd_ms = time_kernels(w)
+    kb = kernel_bytes(w, args)
+    dominant, dom_ms = ("k_raster_bwd", bwd_ms) if bwd_ms >= fwd_ms else ("k_face_setup+k_raster_fwd", fwd_ms)
+    dom_bytes = kb["bwd"] if dominant == "k_raster_bwd" else kb["fwd"] + kb["setup"]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            rec = json.load(open(pmc))
+            if rec.get("config") == [args.batch, args.image_size, args.level, args.mode]:
+                traffic = rec.get("hbm_bytes_per_launch", {}).get(dominant)
+        except Exception:
+            traffic = None
+
+    res = {
+        "metric": "rasterize Mpixels/s fwd+bwd, 256² batch=64; % HBM roofline at 1 & 8 GPU",
+        "value": round(value, 3),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (ico-sphere, jittered per item, random texture atlas)",
+        "config": {"workload": "ico-sphere L%d (V=%d, F=%d), %d items/GPU, %d^2 output (AA, %d^2 internal), %s"
+                               % (args.level, w["V"], w["F"], args.batch, args.image_size, 2 * args.image_size,
+                                  "rgb+sil+depth" if args.mode == "rgbsd" else "silhouettes"),
+                   "global_batch": world * args.batch, "image_size": args.image_size, "faces": w["F"],
+                   "channels": w["C"], "parallelism": "batch-sharded dp%d" % world},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5)},
+        "kernels_ms": {"fwd": round(fwd_ms, 5), "bwd": round(bwd_ms, 5)},
+        "step_roofline_frac": round(kb["total"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+    }
+    if gather_ms is not None:
+        res["gather_ms"] = round(gather_ms, 4)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

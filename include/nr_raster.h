@@ -1,0 +1,131 @@
+/*
+ * nr_raster.h -- C ABI of the MI355X (gfx950) rasterizer library libnr_raster.so.
+ *
+ * Plain pointers (device memory), sizes and a hipStream_t passed as void*.  No torch types.
+ * Every entry point is asynchronous on `stream`, returns 0 on success and a nonzero
+ * NR_ERR_* code on failure, with a message in nr_last_error() (thread-local).  The library never
+ * allocates device memory: callers pass every output and the scratch workspace.
+ *
+ * Reference interfaces replaced (paths relative to /root/reference):
+ *   pybind11 module neural_renderer_torch.cuda.rasterize_cuda  (cuda/rasterize_cuda.cpp:93-99)
+ *     face_index_map_forward_safe  (.cpp:55-65 -> rasterize_cuda_kernel.cu:362-390, kernel :52-153)
+ *                                   -> nr_face_index_map_forward_safe
+ *     compute_weight_map_c         (.cpp:81-90 -> .cu:420-443, kernel :246-308)
+ *                                   -> nr_compute_weight_map
+ *     mask_foreground_forward      (.cpp:35-43 -> .cu:312-335)  -> nr_mask_foreground_forward
+ *     mask_foreground_backward     (.cpp:45-53 -> .cu:337-359)  -> nr_mask_foreground_backward
+ *     face_index_map_forward_unsafe (.cpp:67-79) -- dead code in the reference (its z-buffer
+ *                                   update is commented out, .cu:236-240); not provided.
+ *   python-level stages that had no native code in the reference, fused here:
+ *     rasterize_core forward (rasterize.py:194-329: gather, face index, weight, coordinate, depth,
+ *       texture and silhouette maps, channel merge, flip, 2x2 anti-aliasing)
+ *                                   -> nr_rasterize_forward
+ *     its autograd backward (Differentiation.backward differentiation.py:12-36, MaskForeground,
+ *       to_map index backward, face gather backward)      -> nr_rasterize_backward
+ *     Differentiation.backward on its own (differentiation.py:12-36)
+ *                                   -> nr_differentiation_backward
+ */
+#ifndef NR_RASTER_H_
+#define NR_RASTER_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define NR_API __attribute__((visibility("default")))
+#else
+#define NR_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    NR_OK = 0,
+    NR_ERR_ARGS = 1,    /* invalid sizes / null pointers */
+    NR_ERR_LAUNCH = 2,  /* a HIP launch failed */
+    NR_ERR_WORKSPACE = 3 /* workspace too small */
+};
+
+/* Draw flags for nr_rasterize_forward / nr_rasterize_backward (RasterizeHyperparam.draw_*). */
+enum { NR_DRAW_RGB = 1, NR_DRAW_SILHOUETTES = 2, NR_DRAW_DEPTH = 4 };
+
+NR_API const char* nr_last_error(void);
+NR_API int nr_version(void);
+
+/* Scratch bytes needed by the face-index map for B items, F faces, S x S internal pixels
+ * (per-face screen bounding boxes + coarse-bin face bitmasks). */
+NR_API size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size);
+
+/* rasterize.py:27-38 / rasterize_cuda_kernel.cu:52-153.
+ * faces: [B, F, 3, 3] f32 (screen x, y and depth z of each corner), face_index: [B, S, S] int32
+ * (fully written; -1 = background).  Same arguments and meaning as the reference binding;
+ * `eps` is accepted and unused exactly as in the reference kernel. */
+NR_API int nr_face_index_map_forward_safe(const float* faces, int32_t* face_index, int batch_size, int num_faces,
+                                   int image_size, float near, float far, int draw_backside, float eps,
+                                   float depth_min_delta, void* workspace, size_t workspace_bytes,
+                                   void* stream);
+
+/* rasterize.py:67-77 / .cu:246-308.  weight_map: [B, S, S, 3] f32; background pixels are written
+ * with 0 (the reference relies on a caller-zeroed buffer; here every element is written). */
+NR_API int nr_compute_weight_map(const float* faces, const int32_t* face_index_map, float* weight_map,
+                          int batch_size, int num_faces, int image_size, void* stream);
+
+/* .cu:7-49: copy `dim` floats per pixel where face_index >= 0 (n = number of pixels). */
+NR_API int nr_mask_foreground_forward(const int32_t* face_index, const float* data_in, float* data_out,
+                               long long n, int dim, void* stream);
+NR_API int nr_mask_foreground_backward(const int32_t* face_index, float* grad_in, const float* grad_out,
+                                long long n, int dim, void* stream);
+
+/* differentiation.py:12-36: grad_xy[B, H, W, 2] (x first) from the saved images[B, H, W, C] and
+ * the incoming gradient grad[B, H, W, C]; step = 2 / H as in the reference. */
+NR_API int nr_differentiation_backward(const float* images, const float* grad, float* grad_xy, int batch_size,
+                                int height, int width, int channels, void* stream);
+
+/* Arguments of the fused rasterize_core.  All pointers are device pointers; f32 unless noted.
+ * Strides are in elements; a batch stride of 0 means "shared by every item" (a torch.expand). */
+typedef struct NrRasterArgs {
+    int batch_size;          /* B */
+    int num_vertices;        /* V */
+    int num_faces;           /* F */
+    int image_size;          /* s: output size (RasterizeHyperparam.image_size) */
+    int anti_aliasing;       /* internal S = 2s when set */
+    int draw_backside;
+    int draw_flags;          /* NR_DRAW_* */
+    float near, far, eps;    /* eps: texture-coordinate clamp (RasterizeHyperparam.eps) */
+    float depth_min_delta;   /* 1e-4 in the reference (rasterize.py:35) */
+    const float* vertices;   /* [B, V, 3] contiguous, screen space (after look_at + perspective) */
+    const int32_t* faces;    /* [F, 3] vertex indices, shared by every item */
+    /* textures (only with NR_DRAW_RGB) */
+    const float* vertices_textures; /* [Bvt, Vt, 2]; item stride vt_batch_stride (0 = shared) */
+    long long vt_batch_stride;
+    int num_vertices_textures;
+    const int32_t* faces_textures;  /* [F, 3] */
+    const float* textures;          /* [Bt, 3, H, W] with the strides below; (h, w) row-contiguous */
+    long long tex_stride_b, tex_stride_c, tex_stride_p; /* p = flat texel index h * W + w */
+    int tex_height, tex_width;
+    /* saved state, written by forward, read by backward */
+    float* face_records;     /* [B, F, 9]: gathered faces (rasterize.py:232) */
+    float* face_uv;          /* [Buv, F, 6] with Buv = (vt_batch_stride ? B : 1); only with RGB */
+    int32_t* face_index;     /* [B, S, S] */
+    void* workspace;
+    size_t workspace_bytes;
+} NrRasterArgs;
+
+/* Channels in output order: rgb (3), silhouettes (1), depth (1) -- those enabled by draw_flags. */
+NR_API int nr_num_channels(int draw_flags);
+
+/* rasterize.py:194-329 (without lights / backgrounds): images [B, C, s, s] contiguous. */
+NR_API int nr_rasterize_forward(const NrRasterArgs* args, float* images, void* stream);
+
+/* Backward of nr_rasterize_forward for upstream grad_images [B, C, s, s] (contiguous).
+ * Accumulates (+=) into grad_vertices [B, V, 3] and, with NR_DRAW_RGB and grad_textures != NULL,
+ * grad_textures [Bt, 3, H, W] contiguous, Bt = (tex_stride_b ? B : 1).  Callers zero them first. */
+NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
+                          float* grad_textures, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NR_RASTER_H_ */

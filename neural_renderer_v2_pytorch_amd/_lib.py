@@ -1,0 +1,94 @@
+"""ctypes binding of the HIP library (include/nr_raster.h -> _lib/libnr_raster.so).
+
+The library is loaded on first use.  There is no CPU fallback: if the shared object is missing or
+a call fails, a RuntimeError is raised.  Build it with `python -c "import __graft_entry__ as g;
+g.build()"` from the repository root (hipcc --offload-arch=gfx950).
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libnr_raster.so")
+
+NR_DRAW_RGB = 1
+NR_DRAW_SILHOUETTES = 2
+NR_DRAW_DEPTH = 4
+
+# every symbol declared in include/nr_raster.h
+EXPORTS = [
+    "nr_last_error", "nr_version", "nr_workspace_bytes", "nr_face_index_map_forward_safe",
+    "nr_compute_weight_map", "nr_mask_foreground_forward", "nr_mask_foreground_backward",
+    "nr_differentiation_backward", "nr_num_channels", "nr_rasterize_forward", "nr_rasterize_backward",
+]
+
+c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
+
+
+class NrRasterArgs(ctypes.Structure):
+    _fields_ = [
+        ("batch_size", c_int), ("num_vertices", c_int), ("num_faces", c_int), ("image_size", c_int),
+        ("anti_aliasing", c_int), ("draw_backside", c_int), ("draw_flags", c_int),
+        ("near", c_float), ("far", c_float), ("eps", c_float), ("depth_min_delta", c_float),
+        ("vertices", c_void_p), ("faces", c_void_p),
+        ("vertices_textures", c_void_p), ("vt_batch_stride", c_ll), ("num_vertices_textures", c_int),
+        ("faces_textures", c_void_p), ("textures", c_void_p),
+        ("tex_stride_b", c_ll), ("tex_stride_c", c_ll), ("tex_stride_p", c_ll),
+        ("tex_height", c_int), ("tex_width", c_int),
+        ("face_records", c_void_p), ("face_uv", c_void_p), ("face_index", c_void_p),
+        ("workspace", c_void_p), ("workspace_bytes", c_size_t),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("neural_renderer_v2_pytorch_amd: HIP library %s is missing; build it with "
+                           "__graft_entry__.build() (there is no CPU fallback)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    L.nr_last_error.restype = ctypes.c_char_p
+    L.nr_last_error.argtypes = []
+    L.nr_version.restype = c_int
+    L.nr_workspace_bytes.restype = c_size_t
+    L.nr_workspace_bytes.argtypes = [c_int, c_int, c_int]
+    L.nr_num_channels.restype = c_int
+    L.nr_num_channels.argtypes = [c_int]
+    L.nr_face_index_map_forward_safe.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_int,
+                                                 c_float, c_float, c_void_p, c_size_t, c_void_p]
+    L.nr_compute_weight_map.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
+    L.nr_mask_foreground_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]
+    L.nr_mask_foreground_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]
+    L.nr_differentiation_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
+    L.nr_rasterize_forward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p]
+    L.nr_rasterize_backward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p]
+    for name in EXPORTS:
+        if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels"):
+            getattr(L, name).restype = c_int
+    _lib = L
+    return L
+
+
+def check(status, what):
+    if status != 0:
+        raise RuntimeError("%s failed (status %d): %s" % (what, status, lib().nr_last_error().decode()))
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def require_gpu(*tensors):
+    for t in tensors:
+        if t is not None and (not torch.is_tensor(t) or not t.is_cuda):
+            raise RuntimeError("neural_renderer_v2_pytorch_amd runs on the GPU only (no CPU fallback); "
+                               "got a %s" % ("CPU tensor" if torch.is_tensor(t) else type(t).__name__))

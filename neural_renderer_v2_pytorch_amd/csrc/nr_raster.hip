@@ -1,0 +1,977 @@
+// nr_raster.hip -- MI355X (gfx950 / CDNA4) differentiable mesh rasterizer.
+//
+// Hand-written HIP behind the C ABI of include/nr_raster.h.  Replaces the reference's CUDA
+// extension (neural_renderer_torch/cuda/rasterize_cuda_kernel.cu) AND the torch glue around it in
+// rasterize_core (neural_renderer_torch/rasterize.py:194-329), with the same results:
+//   * face_index_map bit-exact: every pixel scans, in ascending face order, a superset of the faces
+//     whose bounding box contains it, with the reference's float arithmetic unchanged
+//     (rasterize_cuda_kernel.cu:82-149; no FMA contraction, IEEE division, double pixel centres);
+//   * rgb / depth / silhouette values follow rasterize.py:80-153 operation for operation.
+//
+// Pipeline of one forward (3 launches) -- see DESIGN.md for the data layout and rooflines:
+//   k_face_setup     one block per (128 faces, item): gather the faces from vertices (rasterize.py:232),
+//                    per-face screen bbox + face-level rejects, texture-uv gather, and the coarse-bin
+//                    face bitmasks (64x64-pixel bins, bit f set when face f may touch the bin).
+//   k_raster_fwd     one block per 32x8-pixel tile: compacts the coarse bin's faces that touch the
+//                    tile, in face order, into LDS (ballot-free block scan), scans them per pixel,
+//                    then shades rgb/sil/depth and writes fim + the flipped, 2x2-averaged output.
+//   backward         k_raster_bwd: one block per tile with a 1-pixel halo: recomputes the internal
+//                    image from fim, applies Differentiation.backward's stencil, and chains the
+//                    coordinate / depth / texture gradients to vertices and textures with atomics.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <string>
+
+#include "nr_raster.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int TW = 32;             // tile width  (internal pixels)
+constexpr int TH = 8;              // tile height
+constexpr int NT = TW * TH;        // threads per raster block, one pixel each
+constexpr int COARSE = 64;         // coarse bin edge (pixels); multiple of TW and TH
+constexpr int CAP = 256;           // faces staged in LDS per round
+constexpr int SETUP_FACES = 128;   // faces per setup block (4 bitmask words)
+constexpr int MAXC = 5;            // max output channels
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipPeekAtLastError();
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(NR_ERR_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+    }
+    return NR_OK;
+}
+
+struct Geom {
+    int S, nbx, nby, nbins, nwords, tiles_x, tiles_y;
+};
+
+Geom make_geom(int F, int S) {
+    Geom g;
+    g.S = S;
+    g.nbx = (S + COARSE - 1) / COARSE;
+    g.nby = g.nbx;
+    g.nbins = g.nbx * g.nby;
+    g.nwords = (F + 31) / 32;
+    g.tiles_x = (S + TW - 1) / TW;
+    g.tiles_y = (S + TH - 1) / TH;
+    return g;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// workspace layout: [bbox int2 B*F][mask u32 B*nbins*nwords]
+size_t ws_bbox_bytes(int B, int F) { return align_up((size_t)B * F * sizeof(int2)); }
+size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins * g.nwords * 4); }
+
+// ------------------------------------------------------------------------------------------------
+// device helpers
+
+// rasterize_cuda_kernel.cu:76-77: pixel centre, computed in double, rounded to float
+__device__ __forceinline__ float pix_center(int i, int S) { return (float)((2. * i + 1 - S) / S); }
+
+// conservative range of pixel indices whose centre may lie in [lo, hi] (float compare).  Empty
+// when lo > hi.  One pixel of margin on each side absorbs the float rounding of the centres.
+__device__ __forceinline__ void pix_range(float lo, float hi, int S, int& i0, int& i1) {
+    double a = ((double)lo * S + S - 1) * 0.5;
+    double b = ((double)hi * S + S - 1) * 0.5;
+    a = fmin(fmax(a, -2.0), (double)S + 2.0);
+    b = fmin(fmax(b, -2.0), (double)S + 2.0);
+    i0 = max((int)ceil(a) - 1, 0);
+    i1 = min((int)floor(b) + 1, S - 1);
+}
+
+__device__ __forceinline__ int pack_range(int lo, int hi) { return (lo & 0xffff) | (hi << 16); }
+// an empty range never overlaps anything: lo = 32767 > any pixel index, hi = -1
+#define NR_EMPTY_RANGE ((int)0xffff7fff)
+__device__ __forceinline__ int range_lo(int p) { return p & 0xffff; }
+__device__ __forceinline__ int range_hi(int p) { return p >> 16; }
+
+struct Face {
+    float x0, y0, z0, x1, y1, z1, x2, y2, z2;
+};
+
+__device__ __forceinline__ Face load_face(const float* __restrict__ fr) {
+    Face f;
+    f.x0 = fr[0]; f.y0 = fr[1]; f.z0 = fr[2];
+    f.x1 = fr[3]; f.y1 = fr[4]; f.z1 = fr[5];
+    f.x2 = fr[6]; f.y2 = fr[7]; f.z2 = fr[8];
+    return f;
+}
+
+// torch.maximum / torch.minimum / min(-2) / max(-2) semantics: NaN propagates
+__device__ __forceinline__ float t_max(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a > b ? a : b); }
+__device__ __forceinline__ float t_min(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a < b ? a : b); }
+
+// compute_weight_map_cuda_kernel (.cu:286-306)
+__device__ __forceinline__ void face_weights(float xp, float yp, const Face& f, float w[3]) {
+    w[0] = yp * (f.x2 - f.x1) + xp * (f.y1 - f.y2) + (f.x1 * f.y2 - f.x2 * f.y1);
+    w[1] = yp * (f.x0 - f.x2) + xp * (f.y2 - f.y0) + (f.x2 * f.y0 - f.x0 * f.y2);
+    w[2] = yp * (f.x1 - f.x0) + xp * (f.y0 - f.y1) + (f.x0 * f.y1 - f.x1 * f.y0);
+    float s = w[0] + w[1] + w[2];
+    if (s < 0) {
+        w[0] = -w[0];
+        w[1] = -w[1];
+        w[2] = -w[2];
+    }
+    w[0] = fmaxf(w[0], 0.f);
+    w[1] = fmaxf(w[1], 0.f);
+    w[2] = fmaxf(w[2], 0.f);
+    s = w[0] + w[1] + w[2];
+#pragma unroll
+    for (int j = 0; j < 3; j++) w[j] = fmaxf(fminf(w[j] / s, 1.f), 0.f);
+}
+
+struct TexView {
+    const float* __restrict__ tex;
+    long long sb, sc, sp;
+    int H, W;
+};
+
+__device__ __forceinline__ float texel(const TexView& t, int b, int c, int p) {
+    return t.tex[(long long)b * t.sb + (long long)c * t.sc + (long long)p * t.sp];
+}
+
+// sample_textures (rasterize.py:100-153) for one foreground pixel, with the intermediates the
+// backward needs.
+struct TexSample {
+    float zq[3];        // z_k + 1e-10
+    float dt;           // 1 / sum(w/(z+1e-10) + 1e-10)
+    float num[2];       // sum_k (w_k uv_k)/(z_k + 1e-10)
+    float pr[2];        // num * dt (pre-clamp)
+    float pc[2];        // after the lower clamp
+    float hm[2];        // upper bound (max uv - eps)
+    float lo[2];
+    float x, y, x0, y0, x1, y1;
+    int idx[4];
+    float wt[4];
+    float rgb[3];
+};
+
+__device__ __forceinline__ void sample_texture(const Face& f, const float w[3], const float* __restrict__ uv,
+                                               const TexView& tv, int bt, float eps, TexSample& s) {
+    const float z[3] = {f.z0, f.z1, f.z2};
+    float st = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        s.zq[k] = z[k] + 1e-10f;
+        const float t = w[k] / s.zq[k] + 1e-10f;
+        st = (k == 0) ? t : st + t;
+    }
+    s.dt = 1.f / st;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const float u0 = uv[j], u1 = uv[2 + j], u2 = uv[4 + j];
+        s.num[j] = ((w[0] * u0) / s.zq[0] + (w[1] * u1) / s.zq[1]) + (w[2] * u2) / s.zq[2];
+        s.pr[j] = s.num[j] * s.dt;
+        s.lo[j] = t_min(t_min(u0, u1), u2);
+        s.hm[j] = t_max(t_max(u0, u1), u2) - eps;
+        s.pc[j] = t_max(s.pr[j], s.lo[j]);
+    }
+    s.x = t_min(s.pc[0], s.hm[0]);
+    s.y = t_min(s.pc[1], s.hm[1]);
+    s.x0 = floorf(s.x);
+    s.y0 = floorf(s.y);
+    s.x1 = s.x0 + 1;
+    s.y1 = s.y0 + 1;
+    const int xi0 = (int)s.x0, yi0 = (int)s.y0, xi1 = (int)s.x1, yi1 = (int)s.y1;
+    const int W = tv.W, HW = tv.H * tv.W;
+    s.idx[0] = yi0 * W + xi0;
+    s.idx[1] = yi0 * W + xi1;
+    s.idx[2] = yi1 * W + xi0;
+    s.idx[3] = yi1 * W + xi1;
+#pragma unroll
+    for (int i = 0; i < 4; i++) s.idx[i] = min(max(s.idx[i], 0), HW - 1);  // weight-0 overhang, SURVEY A9
+    s.wt[0] = (s.y1 - s.y) * (s.x1 - s.x);
+    s.wt[1] = (s.y1 - s.y) * (s.x - s.x0);
+    s.wt[2] = (s.y - s.y0) * (s.x1 - s.x);
+    s.wt[3] = (s.y - s.y0) * (s.x - s.x0);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const float t0 = texel(tv, bt, c, s.idx[0]), t1 = texel(tv, bt, c, s.idx[1]);
+        const float t2 = texel(tv, bt, c, s.idx[2]), t3 = texel(tv, bt, c, s.idx[3]);
+        s.rgb[c] = ((s.wt[0] * t0 + s.wt[1] * t1) + s.wt[2] * t2) + s.wt[3] * t3;
+    }
+}
+
+// compute_depth_map (rasterize.py:80-88) for a foreground pixel
+__device__ __forceinline__ float depth_value(const Face& f, const float w[3]) {
+    return 1.f / ((w[0] / f.z0 + w[1] / f.z1) + w[2] / f.z2);
+}
+
+struct Shade {
+    int draw;       // NR_DRAW_* flags
+    int C;          // channels
+    float eps;
+    TexView tv;
+    const float* __restrict__ face_uv;
+    long long uv_bstride;  // F*6 or 0
+};
+
+// All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth).
+__device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, float xp, float yp,
+                                            float* out) {
+    int c = 0;
+    if (fi < 0) {
+        for (int k = 0; k < sh.C; k++) out[k] = 0.f;
+        return;
+    }
+    float w[3];
+    face_weights(xp, yp, f, w);
+    if (sh.draw & NR_DRAW_RGB) {
+        TexSample s;
+        const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
+        const int bt = sh.tv.sb ? b : 0;
+        sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
+        out[c++] = s.rgb[0];
+        out[c++] = s.rgb[1];
+        out[c++] = s.rgb[2];
+    }
+    if (sh.draw & NR_DRAW_SILHOUETTES) out[c++] = 1.f;
+    if (sh.draw & NR_DRAW_DEPTH) out[c++] = depth_value(f, w);
+}
+
+// ------------------------------------------------------------------------------------------------
+// block-wide exclusive scan of one int per thread (NT threads, 4 waves)
+__device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds4[wid] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+        const int t = lds4[i];
+        base += (i < wid) ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return base + x - v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_face_setup: per (face group of 128, item)
+//   GATHER: faces come from vertices[b, faces_idx[f, k]] (rasterize.py:232) and are written to
+//           face_records; otherwise face_records already holds the gathered faces (the
+//           face_index_map_forward_safe entry point receives them that way, rasterize.py:34).
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ vertices, const int32_t* __restrict__ faces_idx,
+                                                    float* __restrict__ face_records, int V, int F, int S,
+                                                    int draw_backside, int2* __restrict__ bbox,
+                                                    uint32_t* __restrict__ mask, int nbx, int nbins, int nwords,
+                                                    const float* __restrict__ vt, long long vt_bstride, int Vt,
+                                                    const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
+                                                    int uv_items) {
+    __shared__ int2 s_bb[SETUP_FACES];
+    const int b = blockIdx.y;
+    const int f0 = blockIdx.x * SETUP_FACES;
+    const int t = threadIdx.x;
+    if (t < SETUP_FACES) {
+        const int f = f0 + t;
+        int2 bb = make_int2(NR_EMPTY_RANGE, NR_EMPTY_RANGE);
+        if (f < F) {
+            float c[9];
+            float* rec = face_records + ((long long)b * F + f) * 9;
+            if (GATHER) {
+                const float* vb = vertices + (long long)b * V * 3;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const int vi = faces_idx[f * 3 + k];
+                    c[3 * k + 0] = vb[vi * 3 + 0];
+                    c[3 * k + 1] = vb[vi * 3 + 1];
+                    c[3 * k + 2] = vb[vi * 3 + 2];
+                }
+#pragma unroll
+                for (int k = 0; k < 9; k++) rec[k] = c[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 9; k++) c[k] = rec[k];
+            }
+            const float x0 = c[0], y0 = c[1], x1 = c[3], y1 = c[4], x2 = c[6], y2 = c[7];
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 9; k++) ok = ok && !(c[k] != c[k]);  // NaN faces are never accepted
+            // face-level rejects of .cu:100-104 and .cu:118-121 (pixel independent)
+            if (!draw_backside && (y2 - y0) * (x1 - x0) > (y1 - y0) * (x2 - x0)) ok = false;
+            const float det = x2 * (y0 - y1) + x0 * (y1 - y2) + x1 * (y2 - y0);
+            if ((double)fabsf(det) < 0.00000001) ok = false;
+            if (ok) {
+                int ix0, ix1, iy0, iy1;
+                pix_range(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), S, ix0, ix1);
+                pix_range(fminf(fminf(y0, y1), y2), fmaxf(fmaxf(y0, y1), y2), S, iy0, iy1);
+                if (ix0 <= ix1 && iy0 <= iy1) bb = make_int2(pack_range(ix0, ix1), pack_range(iy0, iy1));
+            }
+            if (face_uv != nullptr && b < uv_items) {
+                const float* vtb = vt + (long long)b * vt_bstride;
+                float* u = face_uv + ((long long)b * F + f) * 6;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const int ti = faces_t[f * 3 + k];
+                    u[2 * k + 0] = vtb[(long long)ti * 2 + 0];
+                    u[2 * k + 1] = vtb[(long long)ti * 2 + 1];
+                }
+            }
+            bbox[(long long)b * F + f] = bb;
+        }
+        s_bb[t] = bb;
+    }
+    __syncthreads();
+    // coarse-bin bitmask words of this face group: (bin, word) pairs
+    const int w0 = blockIdx.x * (SETUP_FACES / 32);
+    const int nw = min(SETUP_FACES / 32, nwords - w0);
+    for (int p = t; p < nbins * nw; p += blockDim.x) {
+        const int bin = p / nw, wi = p % nw;
+        const int bx0 = (bin % nbx) * COARSE, by0 = (bin / nbx) * COARSE;
+        const int bx1 = bx0 + COARSE - 1, by1 = by0 + COARSE - 1;
+        uint32_t bits = 0;
+#pragma unroll 8
+        for (int j = 0; j < 32; j++) {
+            const int2 bb = s_bb[wi * 32 + j];
+            const bool hit = range_lo(bb.x) <= bx1 && range_hi(bb.x) >= bx0 && range_lo(bb.y) <= by1 &&
+                             range_hi(bb.y) >= by0;
+            bits |= (hit ? 1u : 0u) << j;
+        }
+        mask[((long long)b * nbins + bin) * nwords + w0 + wi] = bits;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_raster_fwd: per 32x8 tile.  LDS face record (8 x float4):
+//   0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
+//   4: z2 A B C            | 5: D E F nD      | 6: nF nB k0 k1 | 7: k2 - - -
+struct FwdOut {
+    float* images;   // [B, C, s, s] (FUSED only)
+    int32_t* fim;    // [B, S, S]
+};
+
+__device__ __forceinline__ void pixel_of(int t, int& lx, int& ly) {
+    // 4 waves as a 2x2 grid of 16x4 pixel blocks
+    const int w = t >> 6, l = t & 63;
+    lx = (w & 1) * 16 + (l & 15);
+    ly = (w >> 1) * 4 + (l >> 4);
+}
+
+template <bool FUSED>
+__global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, const int2* __restrict__ bbox,
+                                                  const uint32_t* __restrict__ mask, int F, Geom g, float near,
+                                                  float far, float delta, Shade sh, int aa, FwdOut out) {
+    __shared__ float4 s_face[CAP][8];
+    __shared__ int s_scan[4];
+    __shared__ float s_chan[FUSED ? MAXC : 1][NT];
+
+    const int b = blockIdx.y;
+    const int S = g.S;
+    const int tx0 = (blockIdx.x % g.tiles_x) * TW;
+    const int ty0 = (blockIdx.x / g.tiles_x) * TH;
+    const int t = threadIdx.x;
+    int lx, ly;
+    pixel_of(t, lx, ly);
+    const int px = tx0 + lx, py = ty0 + ly;
+    const float xp = pix_center(px, S);
+    const float yp = pix_center(py, S);
+    // this wave's pixel rectangle, for the wave-uniform face skip
+    const int wave = t >> 6;
+    const int wx0 = tx0 + (wave & 1) * 16, wy0 = ty0 + (wave >> 1) * 4;
+    const int wx1 = wx0 + 15, wy1 = wy0 + 3;
+    const int tx1 = tx0 + TW - 1, ty1 = ty0 + TH - 1;
+
+    float depth_min = far;
+    int best = -1;
+    Face bf = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+    const int bin = (ty0 / COARSE) * g.nbx + (tx0 / COARSE);
+    const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
+    const int2* bbb = bbox + (long long)b * F;
+    const float* frb = face_records + (long long)b * F * 9;
+
+    for (int wbase = 0; wbase < g.nwords; wbase += NT) {
+        const int w = wbase + t;
+        uint32_t bits = (w < g.nwords) ? words[w] : 0u;
+        uint32_t keep = 0;
+        for (uint32_t m = bits; m; m &= m - 1) {
+            const int j = __builtin_ctz(m);
+            const int2 bb = bbb[w * 32 + j];
+            if (range_lo(bb.x) <= tx1 && range_hi(bb.x) >= tx0 && range_lo(bb.y) <= ty1 && range_hi(bb.y) >= ty0)
+                keep |= 1u << j;
+        }
+        int total;
+        const int off = block_scan(__builtin_popcount(keep), total, s_scan);
+        for (int base = 0; base < total; base += CAP) {
+            // stage faces ranked [base, base + CAP) in ascending face order
+            int r = off;
+            for (uint32_t m = keep; m; m &= m - 1, r++) {
+                if (r < base) continue;
+                if (r >= base + CAP) break;
+                const int j = __builtin_ctz(m);
+                const int f = w * 32 + j;
+                const float* c = frb + (long long)f * 9;
+                const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
+                const float x2 = c[6], y2 = c[7], z2 = c[8];
+                const int2 bb = bbb[f];
+                float4* e = s_face[r - base];
+                e[0] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
+                                   fmaxf(fmaxf(y0, y1), y2));
+                e[1] = make_float4(__int_as_float(bb.x), __int_as_float(bb.y), fminf(fminf(z0, z1), z2),
+                                   __int_as_float(f));
+                e[2] = make_float4(x0, y0, x1, y1);
+                e[3] = make_float4(x2, y2, z0, z1);
+                e[4] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
+                e[5] = make_float4(y2 - y1, x0 - x2, y0 - y2, y1 - y2);
+                e[6] = make_float4(y2 - y0, y0 - y1, x1 * y2 - x2 * y1, x2 * y0 - x0 * y2);
+                e[7] = make_float4(x0 * y1 - x1 * y0, 0.f, 0.f, 0.f);
+            }
+            __syncthreads();
+            const int n = min(CAP, total - base);
+            for (int i = 0; i < n; i++) {
+                const float4 q1 = s_face[i][1];
+                const int bx = __float_as_int(q1.x), by = __float_as_int(q1.y);
+                // wave-uniform skip: face bbox misses this wave's 16x4 pixels
+                if (range_lo(bx) > wx1 || range_hi(bx) < wx0 || range_lo(by) > wy1 || range_hi(by) < wy0) continue;
+                const float4 q0 = s_face[i][0];
+                // .cu:94-97 (min/max form, exact for non-NaN faces)
+                if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) continue;
+                const float4 q2 = s_face[i][2], q3 = s_face[i][3], q4 = s_face[i][4], q5 = s_face[i][5];
+                const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
+                // .cu:107-116
+                const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
+                const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
+                if (c1 * c2 < 0) continue;
+                const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
+                if (c2 * c3 < 0) continue;
+                // .cu:124-126
+                if (depth_min < q1.z) continue;
+                const float4 q6 = s_face[i][6], q7 = s_face[i][7];
+                const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
+                // .cu:130-139
+                float w0 = yp * q4.w + xp * q5.w + q6.z;
+                float w1 = yp * q5.y + xp * q6.x + q6.w;
+                float w2 = yp * q4.y + xp * q6.y + q7.x;
+                const float ws = w0 + w1 + w2;
+                w0 /= ws;
+                w1 /= ws;
+                w2 /= ws;
+                const float zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
+                if (zp <= near || far <= zp) continue;
+                if (zp <= depth_min - delta) {  // .cu:145-148
+                    depth_min = zp;
+                    best = __float_as_int(q1.w);
+                    bf.x0 = x0; bf.y0 = y0; bf.z0 = z0;
+                    bf.x1 = x1; bf.y1 = y1; bf.z1 = z1;
+                    bf.x2 = x2; bf.y2 = y2; bf.z2 = z2;
+                }
+            }
+            __syncthreads();
+        }
+    }
+
+    const bool inside = px < S && py < S;
+    if (inside) out.fim[((long long)b * S + py) * S + px] = best;
+    if (!FUSED) return;
+
+    float v[MAXC];
+    shade_pixel(sh, b, best, bf, xp, yp, v);
+    for (int c = 0; c < sh.C; c++) s_chan[c][ly * TW + lx] = v[c];
+    if (!aa) {
+        if (inside) {
+            // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
+            for (int c = 0; c < sh.C; c++)
+                out.images[(((long long)b * sh.C + c) * S + (S - 1 - py)) * S + (S - 1 - px)] = v[c];
+        }
+        return;
+    }
+    __syncthreads();
+    // 2x2 average of the flipped image (rasterize.py:321-328); each output pixel reads
+    // internal (y0..y0+1, x0..x0+1) with y0, x0 even: a=(y0+1,x0+1) b=(y0,x0+1) c=(y0+1,x0) d=(y0,x0)
+    if (t < (TW / 2) * (TH / 2)) {
+        const int ox = t % (TW / 2), oy = t / (TW / 2);
+        const int ix = tx0 + 2 * ox, iy = ty0 + 2 * oy;
+        if (ix < S && iy < S) {
+            const int s = S / 2;
+            const int oi = (S - 2 - iy) / 2, oj = (S - 2 - ix) / 2;
+            const int l00 = (2 * oy) * TW + 2 * ox;
+            for (int c = 0; c < sh.C; c++) {
+                const float a = s_chan[c][l00 + TW + 1], bq = s_chan[c][l00 + 1];
+                const float cq = s_chan[c][l00 + TW], d = s_chan[c][l00];
+                out.images[(((long long)b * sh.C + c) * s + oi) * s + oj] = (((a + bq) + cq) + d) / 4.f;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// compute_weight_map (standalone entry point): one thread per pixel
+__global__ void k_weight_map(const float* __restrict__ faces, const int32_t* __restrict__ fim, float* __restrict__ wm,
+                             int F, int S, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int fi = fim[i];
+    float w[3] = {0.f, 0.f, 0.f};
+    if (fi >= 0) {
+        const long long ss = (long long)S * S;
+        const int bn = (int)(i / ss);
+        const int pn = (int)(i % ss);
+        const Face f = load_face(faces + ((long long)bn * F + fi) * 9);
+        face_weights(pix_center(pn % S, S), pix_center(pn / S, S), f, w);
+    }
+    wm[i * 3 + 0] = w[0];
+    wm[i * 3 + 1] = w[1];
+    wm[i * 3 + 2] = w[2];
+}
+
+__global__ void k_mask_fg(const int32_t* __restrict__ fi, const float* __restrict__ src, float* __restrict__ dst,
+                          long long n, int dim) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || fi[i] < 0) return;
+    for (int j = 0; j < dim; j++) dst[i * dim + j] = src[i * dim + j];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Differentiation.backward stencil (differentiation.py:12-36, utils.py:75-101)
+//   r[i] = -(sum_c (I[i]-I[i+1]) G[i+1]) / step,  l[i] = -(sum_c (I[i+1]-I[i]) G[i]) / step
+//   R[i] = r[i] + r[i-1], L[i] = l[i-1] + l[i] (missing terms 0), then maximum(R, L)
+__device__ __forceinline__ float pair_dot(const float* a, const float* b, const float* g, int C) {
+    float s = (a[0] - b[0]) * g[0];
+    for (int c = 1; c < C; c++) s = s + (a[c] - b[c]) * g[c];
+    return s;
+}
+
+__device__ __forceinline__ float pick_grad(float R, float L) {
+    // utils.maximum: start from L; R > L -> -R; |R-L| < 1e-4 -> 0; max(R, L) <= 0 -> 0
+    float out = (R > L) ? -R : L;
+    if (fabsf(R - L) < 1e-4f) out = 0.f;
+    if (fmaxf(R, L) <= 0.f) out = 0.f;
+    return out;
+}
+
+// grad along one axis at position i of n, given the channel vectors of (i-1, i, i+1)
+__device__ __forceinline__ float axis_grad(const float* Im, const float* I0, const float* Ip, const float* Gm,
+                                           const float* G0, const float* Gp, int i, int n, int C, float step) {
+    const bool has_p = i <= n - 2, has_m = i >= 1;
+    const float r_i = has_p ? -pair_dot(I0, Ip, Gp, C) / step : 0.f;
+    const float r_m = has_m ? -pair_dot(Im, I0, G0, C) / step : 0.f;
+    const float l_i = has_p ? -pair_dot(Ip, I0, G0, C) / step : 0.f;
+    const float l_m = has_m ? -pair_dot(I0, Im, Gm, C) / step : 0.f;
+    return pick_grad(r_i + r_m, l_m + l_i);
+}
+
+__global__ void k_diff_bwd(const float* __restrict__ img, const float* __restrict__ grad, float* __restrict__ gxy, int H,
+                           int W, int C, float step, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const long long hw = (long long)H * W;
+    const int b = (int)(i / hw);
+    const int p = (int)(i % hw);
+    const int y = p / W, x = p % W;
+    auto at = [&](const float* base, int yy, int xx, int c) -> float {
+        return base[(((long long)b * H + yy) * W + xx) * C + c];
+    };
+    // generic-C pair dots without local arrays
+    auto dot = [&](int ya, int xa, int yb, int xb, int yg, int xg) -> float {
+        float s = (at(img, ya, xa, 0) - at(img, yb, xb, 0)) * at(grad, yg, xg, 0);
+        for (int c = 1; c < C; c++) s = s + (at(img, ya, xa, c) - at(img, yb, xb, c)) * at(grad, yg, xg, c);
+        return s;
+    };
+    float gx, gy;
+    {
+        const bool hp = x <= W - 2, hm = x >= 1;
+        const float r_i = hp ? -dot(y, x, y, x + 1, y, x + 1) / step : 0.f;
+        const float r_m = hm ? -dot(y, x - 1, y, x, y, x) / step : 0.f;
+        const float l_i = hp ? -dot(y, x + 1, y, x, y, x) / step : 0.f;
+        const float l_m = hm ? -dot(y, x, y, x - 1, y, x - 1) / step : 0.f;
+        gx = pick_grad(r_i + r_m, l_m + l_i);
+    }
+    {
+        const bool hp = y <= H - 2, hm = y >= 1;
+        const float r_i = hp ? -dot(y, x, y + 1, x, y + 1, x) / step : 0.f;
+        const float r_m = hm ? -dot(y - 1, x, y, x, y, x) / step : 0.f;
+        const float l_i = hp ? -dot(y + 1, x, y, x, y, x) / step : 0.f;
+        const float l_m = hm ? -dot(y, x, y - 1, x, y - 1, x) / step : 0.f;
+        gy = pick_grad(r_i + r_m, l_m + l_i);
+    }
+    gxy[i * 2 + 0] = gx;
+    gxy[i * 2 + 1] = gy;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_raster_bwd: per 32x8 tile with a 1-pixel halo.
+constexpr int HW_ = TW + 2, HH_ = TH + 2, HN = HW_ * HH_;
+
+struct BwdArgs {
+    const float* __restrict__ face_records;
+    const int32_t* __restrict__ fim;
+    const int32_t* __restrict__ faces_idx;
+    const float* __restrict__ grad_images;
+    float* __restrict__ grad_vertices;
+    float* __restrict__ grad_tex;
+    int F, V, aa, s;
+    float step;
+};
+
+__device__ __forceinline__ void upstream_grad(const BwdArgs& a, int C, int b, int y, int x, int S, float* G) {
+    if (a.aa) {
+        const int s = a.s;
+        const int oi = (S - 1 - y) >> 1, oj = (S - 1 - x) >> 1;
+        for (int c = 0; c < C; c++) G[c] = a.grad_images[(((long long)b * C + c) * s + oi) * s + oj] / 4.f;
+    } else {
+        for (int c = 0; c < C; c++)
+            G[c] = a.grad_images[(((long long)b * C + c) * S + (S - 1 - y)) * S + (S - 1 - x)];
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) {
+    __shared__ float s_I[MAXC][HN];
+    __shared__ float s_G[MAXC][HN];
+    const int b = blockIdx.y;
+    const int S = g.S;
+    const int C = sh.C;
+    const int tx0 = (blockIdx.x % g.tiles_x) * TW;
+    const int ty0 = (blockIdx.x / g.tiles_x) * TH;
+    const int t = threadIdx.x;
+    int lx, ly;
+    pixel_of(t, lx, ly);
+    const int px = tx0 + lx, py = ty0 + ly;
+    const bool inside = px < S && py < S;
+    const float xp = pix_center(px, S), yp = pix_center(py, S);
+
+    int fi = -1;
+    Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float I[MAXC], G[MAXC];
+    for (int c = 0; c < MAXC; c++) I[c] = G[c] = 0.f;
+    if (inside) {
+        fi = a.fim[((long long)b * S + py) * S + px];
+        if (fi >= 0) f = load_face(a.face_records + ((long long)b * a.F + fi) * 9);
+        shade_pixel(sh, b, fi, f, xp, yp, I);
+        upstream_grad(a, C, b, py, px, S, G);
+    }
+    const int li = (ly + 1) * HW_ + (lx + 1);
+    for (int c = 0; c < C; c++) {
+        s_I[c][li] = I[c];
+        s_G[c][li] = G[c];
+    }
+    // halo ring: 2 rows of HW_ + 2 columns of TH
+    if (t < 2 * HW_ + 2 * TH) {
+        int hx, hy;
+        if (t < HW_) { hy = 0; hx = t; }
+        else if (t < 2 * HW_) { hy = HH_ - 1; hx = t - HW_; }
+        else if (t < 2 * HW_ + TH) { hy = 1 + (t - 2 * HW_); hx = 0; }
+        else { hy = 1 + (t - 2 * HW_ - TH); hx = HW_ - 1; }
+        const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+        float hI[MAXC], hG[MAXC];
+        for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
+        if (y >= 0 && y < S && x >= 0 && x < S) {
+            const int hf = a.fim[((long long)b * S + y) * S + x];
+            Face ff = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            if (hf >= 0) ff = load_face(a.face_records + ((long long)b * a.F + hf) * 9);
+            shade_pixel(sh, b, hf, ff, pix_center(x, S), pix_center(y, S), hI);
+            upstream_grad(a, C, b, y, x, S, hG);
+        }
+        const int hl = hy * HW_ + hx;
+        for (int c = 0; c < C; c++) {
+            s_I[c][hl] = hI[c];
+            s_G[c][hl] = hG[c];
+        }
+    }
+    __syncthreads();
+    if (!inside || fi < 0) return;
+
+    // Differentiation.backward at this pixel
+    float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
+    for (int c = 0; c < C; c++) {
+        Im[c] = s_I[c][li - 1]; Ip[c] = s_I[c][li + 1];
+        Gm[c] = s_G[c][li - 1]; Gp[c] = s_G[c][li + 1];
+    }
+    const float gx = axis_grad(Im, I, Ip, Gm, G, Gp, px, S, C, a.step);
+    for (int c = 0; c < C; c++) {
+        Im[c] = s_I[c][li - HW_]; Ip[c] = s_I[c][li + HW_];
+        Gm[c] = s_G[c][li - HW_]; Gp[c] = s_G[c][li + HW_];
+    }
+    const float gy = axis_grad(Im, I, Ip, Gm, G, Gp, py, S, C, a.step);
+
+    float w[3];
+    face_weights(xp, yp, f, w);
+    // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
+    float gF[3][3];
+    for (int k = 0; k < 3; k++) {
+        gF[k][0] = gx * w[k];
+        gF[k][1] = gy * w[k];
+        gF[k][2] = 0.f;
+    }
+    const float z[3] = {f.z0, f.z1, f.z2};
+    int c = 0;
+    if (sh.draw & NR_DRAW_RGB) {
+        TexSample s;
+        const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
+        const int bt = sh.tv.sb ? b : 0;
+        sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
+        const float gc[3] = {G[0], G[1], G[2]};
+        c = 3;
+        // bilinear: images = sum_i wt_i T_i  -> textures and weights
+        float gw[4];
+        const int HWt = sh.tv.H * sh.tv.W;
+        for (int i = 0; i < 4; i++) {
+            float acc = 0.f;
+            for (int ch = 0; ch < 3; ch++) {
+                const float tv = texel(sh.tv, bt, ch, s.idx[i]);
+                acc = (ch == 0) ? gc[ch] * tv : acc + gc[ch] * tv;
+                const float gt = gc[ch] * s.wt[i];
+                if (a.grad_tex && gt != 0.f) unsafeAtomicAdd(a.grad_tex + ((long long)bt * 3 + ch) * HWt + s.idx[i], gt);
+            }
+            gw[i] = acc;
+        }
+        const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
+        float g_x = -(gw[0] * ay);
+        g_x = g_x + gw[1] * ay;
+        g_x = g_x - gw[2] * by;
+        g_x = g_x + gw[3] * by;
+        float g_y = -(gw[0] * ax);
+        g_y = g_y - gw[1] * bx;
+        g_y = g_y + gw[2] * ax;
+        g_y = g_y + gw[3] * bx;
+        const float gp[2] = {g_x, g_y};
+        float gpr[2];
+        for (int j = 0; j < 2; j++) {
+            // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
+            const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
+            float gg = gp[j];
+            gg = (pc == hm) ? gg / 2 : (pc > hm ? 0.f : gg);
+            gg = (pr == lo) ? gg / 2 : (pr < lo ? 0.f : gg);
+            gpr[j] = gg;
+        }
+        const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
+        const float g_st = -g_dt * (s.dt * s.dt);
+        const float* fuv2 = fuv;
+        for (int k = 0; k < 3; k++) {
+            float gz = 0.f;
+            for (int j = 0; j < 2; j++) {
+                const float p = w[k] * fuv2[2 * k + j];
+                gz = gz + (-(gpr[j] * s.dt)) * ((p / s.zq[k]) / s.zq[k]);
+            }
+            gz = gz + (-g_st) * ((w[k] / s.zq[k]) / s.zq[k]);
+            gF[k][2] += gz;
+        }
+    }
+    if (sh.draw & NR_DRAW_SILHOUETTES) c++;
+    if (sh.draw & NR_DRAW_DEPTH) {
+        const float gd = G[c];
+        const float d = I[c];
+        const float g_s = -gd * (d * d);
+        for (int k = 0; k < 3; k++) gF[k][2] += (-g_s) * ((w[k] / z[k]) / z[k]);
+    }
+    // faces = vertices[:, faces] backward: scatter to the three corner vertices
+    float* gv = a.grad_vertices + (long long)b * a.V * 3;
+    for (int k = 0; k < 3; k++) {
+        const int vi = a.faces_idx[fi * 3 + k];
+        if (gF[k][0] != 0.f) unsafeAtomicAdd(gv + vi * 3 + 0, gF[k][0]);
+        if (gF[k][1] != 0.f) unsafeAtomicAdd(gv + vi * 3 + 1, gF[k][1]);
+        if (gF[k][2] != 0.f) unsafeAtomicAdd(gv + vi * 3 + 2, gF[k][2]);
+    }
+}
+
+int validate_raster(const NrRasterArgs* a, bool need_workspace) {
+    if (!a) return fail(NR_ERR_ARGS, "null args");
+    if (a->batch_size < 0 || a->num_faces < 0 || a->num_vertices < 0 || a->image_size <= 0)
+        return fail(NR_ERR_ARGS, "bad sizes B=%d F=%d V=%d s=%d", a->batch_size, a->num_faces, a->num_vertices,
+                    a->image_size);
+    const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
+    if (S > 16384) return fail(NR_ERR_ARGS, "image too large (%d internal pixels per side)", S);
+    if (nr_num_channels(a->draw_flags) == 0) return fail(NR_ERR_ARGS, "nothing to draw");
+    if (a->batch_size > 0 && a->num_faces > 0 && (!a->vertices || !a->faces || !a->face_records))
+        return fail(NR_ERR_ARGS, "null vertices/faces/face_records");
+    if (a->batch_size > 0 && !a->face_index) return fail(NR_ERR_ARGS, "null face_index");
+    if (a->draw_flags & NR_DRAW_RGB) {
+        if (!a->vertices_textures || !a->faces_textures || !a->textures || !a->face_uv)
+            return fail(NR_ERR_ARGS, "rgb requested without textures");
+        if (a->tex_height <= 0 || a->tex_width <= 0) return fail(NR_ERR_ARGS, "bad texture size");
+    }
+    const Geom g = make_geom(a->num_faces, S);
+    if (need_workspace && (!a->workspace || a->workspace_bytes < ws_bbox_bytes(a->batch_size, a->num_faces) +
+                                                                  ws_mask_bytes(a->batch_size, g)))
+        return fail(NR_ERR_WORKSPACE, "workspace missing or too small");
+    return NR_OK;
+}
+
+Shade make_shade(const NrRasterArgs* a) {
+    Shade sh;
+    sh.draw = a->draw_flags;
+    sh.C = nr_num_channels(a->draw_flags);
+    sh.eps = a->eps;
+    sh.tv.tex = a->textures;
+    sh.tv.sb = a->tex_stride_b;
+    sh.tv.sc = a->tex_stride_c;
+    sh.tv.sp = a->tex_stride_p;
+    sh.tv.H = a->tex_height;
+    sh.tv.W = a->tex_width;
+    sh.face_uv = a->face_uv;
+    sh.uv_bstride = a->vt_batch_stride ? (long long)a->num_faces * 6 : 0;
+    return sh;
+}
+
+}  // namespace
+
+// ==================================================================================================
+extern "C" {
+
+const char* nr_last_error(void) { return g_err.c_str(); }
+int nr_version(void) { return 1; }
+
+int nr_num_channels(int draw_flags) {
+    return ((draw_flags & NR_DRAW_RGB) ? 3 : 0) + ((draw_flags & NR_DRAW_SILHOUETTES) ? 1 : 0) +
+           ((draw_flags & NR_DRAW_DEPTH) ? 1 : 0);
+}
+
+size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
+    const Geom g = make_geom(num_faces, image_size);
+    return ws_bbox_bytes(batch_size, num_faces) + ws_mask_bytes(batch_size, g);
+}
+
+static int run_face_index(const float* vertices, const int32_t* faces_idx, float* face_records, int32_t* fim,
+                          int B, int V, int F, int S, float near, float far, int draw_backside, float delta,
+                          void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images) {
+    const Geom g = make_geom(F, S);
+    int2* bbox = (int2*)ws;
+    uint32_t* mask = (uint32_t*)((char*)ws + ws_bbox_bytes(B, F));
+    if (B == 0) return NR_OK;
+    if (F > 0) {
+        dim3 grid((F + SETUP_FACES - 1) / SETUP_FACES, B);
+        const bool rgb = ra && (ra->draw_flags & NR_DRAW_RGB);
+        const int uv_items = rgb ? (ra->vt_batch_stride ? B : 1) : 0;
+        if (vertices)
+            hipLaunchKernelGGL(k_face_setup<true>, grid, dim3(256), 0, st, vertices, faces_idx, face_records, V, F, S,
+                               draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
+                               rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
+                               rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
+                               rgb ? ra->face_uv : nullptr, uv_items);
+        else
+            hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), 0, st, nullptr, nullptr, face_records, V, F, S,
+                               draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0);
+        int e = check_launch("k_face_setup");
+        if (e) return e;
+    }
+    FwdOut out;
+    out.fim = fim;
+    out.images = images;
+    dim3 grid(g.tiles_x * g.tiles_y, B);
+    if (ra) {
+        Shade sh = make_shade(ra);
+        hipLaunchKernelGGL(k_raster_fwd<true>, grid, dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far, delta,
+                           sh, ra->anti_aliasing, out);
+    } else {
+        Shade sh = {};
+        hipLaunchKernelGGL(k_raster_fwd<false>, grid, dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far, delta,
+                           sh, 0, out);
+    }
+    return check_launch("k_raster_fwd");
+}
+
+int nr_face_index_map_forward_safe(const float* faces, int32_t* face_index, int batch_size, int num_faces,
+                                   int image_size, float near, float far, int draw_backside, float eps,
+                                   float depth_min_delta, void* workspace, size_t workspace_bytes, void* stream) {
+    (void)eps;
+    if (batch_size < 0 || num_faces < 0 || image_size <= 0 || image_size > 16384)
+        return fail(NR_ERR_ARGS, "bad sizes B=%d F=%d S=%d", batch_size, num_faces, image_size);
+    if (batch_size > 0 && (!face_index || (num_faces > 0 && !faces))) return fail(NR_ERR_ARGS, "null pointer");
+    if (workspace_bytes < nr_workspace_bytes(batch_size, num_faces, image_size))
+        return fail(NR_ERR_WORKSPACE, "workspace too small");
+    return run_face_index(nullptr, nullptr, const_cast<float*>(faces), face_index, batch_size, 0, num_faces,
+                          image_size, near, far, draw_backside, depth_min_delta, workspace, workspace_bytes,
+                          (hipStream_t)stream, nullptr, nullptr);
+}
+
+int nr_compute_weight_map(const float* faces, const int32_t* face_index_map, float* weight_map, int batch_size,
+                          int num_faces, int image_size, void* stream) {
+    if (batch_size < 0 || num_faces < 0 || image_size <= 0) return fail(NR_ERR_ARGS, "bad sizes");
+    const long long n = (long long)batch_size * image_size * image_size;
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(k_weight_map, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, faces,
+                       face_index_map, weight_map, num_faces, image_size, n);
+    return check_launch("k_weight_map");
+}
+
+int nr_mask_foreground_forward(const int32_t* face_index, const float* data_in, float* data_out, long long n, int dim,
+                               void* stream) {
+    if (n < 0 || dim < 0) return fail(NR_ERR_ARGS, "bad sizes");
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(k_mask_fg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, face_index,
+                       data_in, data_out, n, dim);
+    return check_launch("k_mask_fg");
+}
+
+int nr_mask_foreground_backward(const int32_t* face_index, float* grad_in, const float* grad_out, long long n, int dim,
+                                void* stream) {
+    return nr_mask_foreground_forward(face_index, grad_out, grad_in, n, dim, stream);
+}
+
+int nr_differentiation_backward(const float* images, const float* grad, float* grad_xy, int batch_size, int height,
+                                int width, int channels, void* stream) {
+    if (batch_size < 0 || height <= 0 || width <= 0 || channels <= 0) return fail(NR_ERR_ARGS, "bad sizes");
+    const long long n = (long long)batch_size * height * width;
+    if (n == 0) return NR_OK;
+    const float step = (float)(2. / height);
+    hipLaunchKernelGGL(k_diff_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, images, grad,
+                       grad_xy, height, width, channels, step, n);
+    return check_launch("k_diff_bwd");
+}
+
+int nr_rasterize_forward(const NrRasterArgs* a, float* images, void* stream) {
+    int e = validate_raster(a, true);
+    if (e) return e;
+    if (!images && a->batch_size > 0) return fail(NR_ERR_ARGS, "null images");
+    const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
+    return run_face_index(a->vertices, a->faces, a->face_records, a->face_index, a->batch_size, a->num_vertices,
+                          a->num_faces, S, a->near, a->far, a->draw_backside, a->depth_min_delta, a->workspace,
+                          a->workspace_bytes, (hipStream_t)stream, a, images);
+}
+
+int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float* grad_vertices, float* grad_textures,
+                          void* stream) {
+    int e = validate_raster(a, false);
+    if (e) return e;
+    if (a->batch_size == 0) return NR_OK;
+    if (!grad_images || !grad_vertices) return fail(NR_ERR_ARGS, "null gradient buffers");
+    const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
+    const Geom g = make_geom(a->num_faces, S);
+    BwdArgs ba;
+    ba.face_records = a->face_records;
+    ba.fim = a->face_index;
+    ba.faces_idx = a->faces;
+    ba.grad_images = grad_images;
+    ba.grad_vertices = grad_vertices;
+    ba.grad_tex = (a->draw_flags & NR_DRAW_RGB) ? grad_textures : nullptr;
+    ba.F = a->num_faces;
+    ba.V = a->num_vertices;
+    ba.aa = a->anti_aliasing;
+    ba.s = a->image_size;
+    ba.step = (float)(2. / S);
+    Shade sh = make_shade(a);
+    hipLaunchKernelGGL(k_raster_bwd, dim3(g.tiles_x * g.tiles_y, a->batch_size), dim3(NT), 0, (hipStream_t)stream, ba,
+                       g, sh);
+    return check_launch("k_raster_bwd");
+}
+
+}  // extern "C"

@@ -1,0 +1,350 @@
+"""Rasterize API -- drop-in for neural_renderer_torch.rasterize (reference rasterize.py:1-365).
+
+Public surface kept: rasterize_silhouettes / rasterize_rgba / rasterize_rgb / rasterize_depth
+(rasterize.py:332-365), rasterize_core (:194-329), FaceIndexMap / compute_face_index_map (:14-64),
+compute_weight_map (:67-77), RasterizeParam / RasterizeHyperparam.
+
+What changed underneath: rasterize_core is one autograd Function, `Rasterize`, whose forward and
+backward are two calls into the HIP library (csrc/nr_raster.hip through include/nr_raster.h):
+no per-batch Python loops, no host<->device copies, no intermediate [B,S,S,*] maps in HBM.
+
+Behavioural notes ("Drop-in boundary"):
+  * like the reference, the wrappers set hyperparams.draw_* on the object they are given; unlike
+    the reference, rasterize_core does NOT double hyperparams.image_size in place under
+    anti-aliasing (rasterize.py:227-228 compounds on every reuse of the object);
+  * lights (rasterize.py:252-283) and backgrounds (:208-226, :286-288) raise NotImplementedError
+    (SURVEY.md section 8f "next" rows; the reference's own blend_backgrounds raises AttributeError
+    at rasterize.py:157);
+  * gradients flow to vertices and textures; a vertices_textures tensor that requires grad is
+    rejected (NotImplementedError) rather than silently given no gradient.
+"""
+import torch
+
+from . import _lib
+from .rasterize_param import RasterizeParam, RasterizeHyperparam  # noqa: F401  (re-exported like the reference)
+
+
+# ------------------------------------------------------------------------------------------------
+# the face-index and weight kernels on their own (reference rasterize.py:14-77)
+class FaceIndexMap(torch.nn.Module):
+    """Z-buffered face index per internal pixel: [B, F, 3, 3] faces -> int32 [B, S, S]
+    (-1 = background).  rasterize.py:14-57 / rasterize_cuda_kernel.cu:52-153."""
+
+    def __init__(self, num_faces, image_size, near, far, draw_backside):
+        super().__init__()
+        self.num_faces = num_faces
+        self.image_size = image_size
+        self.near = near
+        self.far = far
+        self.draw_backside = draw_backside
+
+    def forward(self, inputs, **kwargs):
+        return self.forward_gpu_safe(inputs)
+
+    def forward_gpu_safe(self, inputs):
+        faces = inputs
+        _lib.require_gpu(faces)
+        faces = faces.detach().contiguous().float()
+        B = faces.shape[0]
+        S = int(self.image_size)
+        fim = torch.empty((B, S, S), dtype=torch.int32, device=faces.device)
+        ws = torch.empty(_lib.lib().nr_workspace_bytes(B, int(self.num_faces), S), dtype=torch.uint8,
+                         device=faces.device)
+        with torch.cuda.device(faces.device):
+            _lib.check(_lib.lib().nr_face_index_map_forward_safe(
+                _lib.ptr(faces), _lib.ptr(fim), B, int(self.num_faces), S, float(self.near), float(self.far),
+                int(self.draw_backside), 1e-8, 1e-4, _lib.ptr(ws), ws.numel(), _lib.stream_of(faces)),
+                "nr_face_index_map_forward_safe")
+        return fim
+
+
+def compute_face_index_map(faces, hyperparams):
+    return FaceIndexMap(faces.shape[1], hyperparams.image_size, hyperparams.near, hyperparams.far,
+                        hyperparams.draw_backside)(faces)
+
+
+def compute_weight_map(faces, face_index_map):
+    """Barycentric weights of the visible face per pixel, [B, S, S, 3] (rasterize.py:67-77)."""
+    _lib.require_gpu(faces, face_index_map)
+    faces = faces.detach().contiguous().float()
+    fim = face_index_map.contiguous().to(torch.int32)
+    B, F = faces.shape[:2]
+    S = fim.shape[1]
+    w = torch.empty((B, S, S, 3), dtype=torch.float32, device=faces.device)
+    with torch.cuda.device(faces.device):
+        _lib.check(_lib.lib().nr_compute_weight_map(_lib.ptr(faces), _lib.ptr(fim), _lib.ptr(w), B, F, S,
+                                                    _lib.stream_of(faces)), "nr_compute_weight_map")
+    return w
+
+
+class MaskForeground(torch.autograd.Function):
+    """utils.MaskForeground (utils.py:117-156): keep foreground pixels, zero elsewhere."""
+
+    @staticmethod
+    def forward(ctx, data_in, face_index_map):
+        _lib.require_gpu(data_in, face_index_map)
+        data_in = data_in.contiguous().float()
+        fim = face_index_map.contiguous().to(torch.int32)
+        out = torch.zeros_like(data_in)
+        n = fim.numel()
+        dim = data_in.numel() // max(n, 1)
+        with torch.cuda.device(data_in.device):
+            _lib.check(_lib.lib().nr_mask_foreground_forward(_lib.ptr(fim), _lib.ptr(data_in), _lib.ptr(out), n, dim,
+                                                             _lib.stream_of(data_in)), "nr_mask_foreground_forward")
+        ctx.save_for_backward(fim)
+        ctx.dim = dim
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        fim, = ctx.saved_tensors
+        grad = grad.contiguous()
+        gin = torch.zeros_like(grad)
+        with torch.cuda.device(grad.device):
+            _lib.check(_lib.lib().nr_mask_foreground_backward(_lib.ptr(fim), _lib.ptr(gin), _lib.ptr(grad), fim.numel(),
+                                                              ctx.dim, _lib.stream_of(grad)), "nr_mask_foreground_backward")
+        return gin, None
+
+
+def mask_foreground(data, face_index_map):
+    return MaskForeground.apply(data, face_index_map)
+
+
+# ------------------------------------------------------------------------------------------------
+# the fused path
+_faces_checked = {}
+
+
+def _faces_i32(faces, device, bound, what):
+    """[F,3] int32 on `device`, indices checked like the reference's IndexError on out-of-range
+    indices (rasterize.py:232, :246).  CPU index tensors are checked on the host before the copy;
+    device-resident int32 ones once per (storage, version), so steady-state calls never sync."""
+    f = torch.as_tensor(faces)
+    if f.ndim != 2 or f.shape[1] != 3:
+        raise AssertionError("%s must be [F, 3]" % what)
+    if not f.is_cuda:
+        if f.numel():
+            lo, hi = int(f.min()), int(f.max())
+            if lo < 0 or hi >= bound:
+                raise IndexError("%s index out of range [0, %d): min %d max %d" % (what, bound, lo, hi))
+        return f.to(dtype=torch.int32).contiguous().to(device, non_blocking=False)
+    reuse = f.dtype == torch.int32 and f.is_contiguous() and f.device == device
+    f = f.to(device=device, dtype=torch.int32).contiguous()
+    key = (f.data_ptr(), f._version, f.shape[0], bound)
+    if f.numel() and not (reuse and _faces_checked.get(what) == key):
+        lo, hi = int(f.min()), int(f.max())
+        if lo < 0 or hi >= bound:
+            raise IndexError("%s index out of range [0, %d): min %d max %d" % (what, bound, lo, hi))
+        if reuse:
+            _faces_checked[what] = key
+    return f
+
+
+class _Cfg:
+    __slots__ = ("image_size", "aa", "backside", "flags", "near", "far", "eps", "C", "V", "F", "tex_shared",
+                 "tex_hw", "vt_shared", "Vt", "B")
+
+
+def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws):
+    a = _lib.NrRasterArgs()
+    a.batch_size = cfg.B
+    a.num_vertices = cfg.V
+    a.num_faces = cfg.F
+    a.image_size = cfg.image_size
+    a.anti_aliasing = int(cfg.aa)
+    a.draw_backside = int(cfg.backside)
+    a.draw_flags = cfg.flags
+    a.near = cfg.near
+    a.far = cfg.far
+    a.eps = cfg.eps
+    a.depth_min_delta = 1e-4
+    a.vertices = vertices.data_ptr()
+    a.faces = faces.data_ptr()
+    a.face_records = face_records.data_ptr()
+    a.face_index = fim.data_ptr()
+    if ws is not None:
+        a.workspace = ws.data_ptr()
+        a.workspace_bytes = ws.numel()
+    else:  # the backward does not use the workspace
+        a.workspace = None
+        a.workspace_bytes = 0
+    if cfg.flags & _lib.NR_DRAW_RGB:
+        a.vertices_textures = vt.data_ptr()
+        a.vt_batch_stride = vt.stride(0)
+        a.num_vertices_textures = cfg.Vt
+        a.faces_textures = ft.data_ptr()
+        a.textures = tex.data_ptr()
+        a.tex_stride_b = tex.stride(0)
+        a.tex_stride_c = tex.stride(1)
+        a.tex_stride_p = tex.stride(3)
+        a.tex_height, a.tex_width = cfg.tex_hw
+        a.face_uv = face_uv.data_ptr()
+    return a
+
+
+class Rasterize(torch.autograd.Function):
+    """rasterize_core (rasterize.py:194-329) as one Function: vertices [B,V,3] (+ textures) ->
+    images [B, C, s, s]; backward returns d/dvertices and d/dtextures."""
+
+    @staticmethod
+    def forward(ctx, vertices, textures, vertices_textures, faces, faces_textures, cfg):
+        dev = vertices.device
+        B = cfg.B
+        S = cfg.image_size * (2 if cfg.aa else 1)
+        L = _lib.lib()
+        fim = torch.empty((B, S, S), dtype=torch.int32, device=dev)
+        face_records = torch.empty((B, cfg.F, 9), dtype=torch.float32, device=dev)
+        rgb = bool(cfg.flags & _lib.NR_DRAW_RGB)
+        face_uv = None
+        if rgb:
+            uv_items = 1 if vertices_textures.stride(0) == 0 else B
+            face_uv = torch.empty((uv_items, cfg.F, 6), dtype=torch.float32, device=dev)
+        ws = torch.empty(L.nr_workspace_bytes(B, cfg.F, S), dtype=torch.uint8, device=dev)
+        images = torch.empty((B, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev)
+        a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws)
+        with torch.cuda.device(dev):
+            _lib.check(L.nr_rasterize_forward(a, _lib.ptr(images), _lib.stream_of(vertices)), "nr_rasterize_forward")
+        ctx.cfg = cfg
+        ctx.save_for_backward(vertices, textures, vertices_textures, faces, faces_textures, face_records, face_uv,
+                              fim)
+        ctx.mark_non_differentiable(fim)
+        return images, fim
+
+    @staticmethod
+    def backward(ctx, grad_images, _grad_fim):
+        cfg = ctx.cfg
+        vertices, textures, vt, faces, ft, face_records, face_uv, fim = ctx.saved_tensors
+        grad_images = grad_images.contiguous()
+        gv = torch.zeros_like(vertices)
+        gt = None
+        want_tex = bool(cfg.flags & _lib.NR_DRAW_RGB) and ctx.needs_input_grad[1]
+        if want_tex:
+            H, W = cfg.tex_hw
+            gt = torch.zeros((1 if cfg.tex_shared else cfg.B, 3, H, W), dtype=torch.float32, device=vertices.device)
+        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None)
+        with torch.cuda.device(vertices.device):
+            _lib.check(_lib.lib().nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt),
+                                                         _lib.stream_of(vertices)), "nr_rasterize_backward")
+        if gt is not None and cfg.tex_shared and cfg.B > 1:
+            # textures is a batch-expanded view: its gradient is summed over the batch by the
+            # expand's backward; hand back the batch total spread evenly
+            gt = (gt / cfg.B).expand(textures.shape)
+        return (gv if ctx.needs_input_grad[0] else None), gt, None, None, None, None
+
+
+def _flags(hp):
+    return ((_lib.NR_DRAW_RGB if hp.draw_rgb else 0) | (_lib.NR_DRAW_SILHOUETTES if hp.draw_silhouettes else 0) |
+            (_lib.NR_DRAW_DEPTH if hp.draw_depth else 0))
+
+
+def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: RasterizeHyperparam, return_face_index=False):
+    """Render [B, C, s, s] images (channels rgb, silhouettes, depth in that order, those enabled
+    by hyperparams.draw_*).  Same contract as rasterize.py:194-329."""
+    assert vertices.ndim == 3
+    assert vertices.shape[2] == 3
+    faces_t = torch.as_tensor(faces)
+    assert faces_t.ndim == 2
+    assert faces_t.shape[1] == 3
+    if hyperparams.draw_rgb:
+        assert params.vertices_textures.ndim == 3
+        assert params.vertices_textures.shape[2] == 2
+        assert torch.as_tensor(params.faces_textures).ndim == 2
+        assert params.faces_textures.shape[1] == 3
+        assert params.textures.ndim == 4
+        assert params.textures.shape[1] == 3
+    if params.backgrounds is not None:  # shape contract of rasterize.py:216-225
+        assert params.backgrounds.ndim == 4
+        assert params.backgrounds.shape[0] == vertices.shape[0]
+        assert params.backgrounds.shape[1] == 3
+        side = hyperparams.image_size * (2 if hyperparams.anti_aliasing else 1)
+        assert params.backgrounds.shape[2] == side and params.backgrounds.shape[3] == side
+    if params.lights is not None and hyperparams.draw_rgb:
+        raise NotImplementedError("lights (rasterize.py:252-283) are not implemented on the MI355X path yet")
+    if (params.backgrounds is not None or params.background_color is not None) and hyperparams.draw_rgb:
+        raise NotImplementedError("background blending (rasterize.py:156-159, 286-288) is not implemented; the "
+                                  "reference's torch blend_backgrounds raises AttributeError there")
+    flags = _flags(hyperparams)
+    if flags == 0:
+        raise Exception  # rasterize.py:309-310
+    _lib.require_gpu(vertices)
+    dev = vertices.device
+    v = vertices.float().contiguous()
+    cfg = _Cfg()
+    cfg.B, cfg.V = v.shape[0], v.shape[1]
+    cfg.F = faces_t.shape[0]
+    cfg.image_size = int(hyperparams.image_size)
+    cfg.aa = bool(hyperparams.anti_aliasing)
+    cfg.backside = bool(hyperparams.draw_backside)
+    cfg.flags = flags
+    cfg.near, cfg.far, cfg.eps = float(hyperparams.near), float(hyperparams.far), float(hyperparams.eps)
+    cfg.C = _lib.lib().nr_num_channels(flags)
+    fi = _faces_i32(faces_t, dev, cfg.V, "faces")
+    tex = vt = ft = None
+    cfg.tex_shared = cfg.vt_shared = False
+    cfg.tex_hw = (0, 0)
+    cfg.Vt = 0
+    if hyperparams.draw_rgb:
+        vt = params.vertices_textures
+        tex = params.textures
+        _lib.require_gpu(vt, tex)
+        if vt.requires_grad:
+            raise NotImplementedError("gradients w.r.t. vertices_textures are not implemented")
+        vt = vt.detach().float()
+        if vt.shape[0] not in (1, cfg.B):
+            raise AssertionError("vertices_textures batch must be 1 or %d" % cfg.B)
+        if vt.shape[0] == 1 and cfg.B > 1:
+            vt = vt.expand(cfg.B, *vt.shape[1:])
+        if vt.stride(2) != 1 or vt.stride(1) != 2:
+            vt = vt.contiguous()
+        cfg.Vt = vt.shape[1]
+        cfg.vt_shared = vt.stride(0) == 0
+        ft = _faces_i32(params.faces_textures, dev, cfg.Vt, "faces_textures")
+        if ft.shape[0] != cfg.F:
+            raise AssertionError("faces_textures must have one row per face")
+        tex = tex.float()
+        if tex.shape[0] not in (1, cfg.B):
+            raise AssertionError("textures batch must be 1 or %d" % cfg.B)
+        if tex.shape[0] == 1 and cfg.B > 1:
+            tex = tex.expand(cfg.B, *tex.shape[1:])
+        H, W = tex.shape[2], tex.shape[3]
+        if tex.stride(2) != W * tex.stride(3):
+            tex = tex.contiguous()
+        cfg.tex_hw = (H, W)
+        cfg.tex_shared = tex.stride(0) == 0 or cfg.B == 1
+    else:
+        tex = torch.empty(0, device=dev)
+    if vt is None:
+        vt = torch.empty(0, device=dev)
+        ft = torch.empty(0, dtype=torch.int32, device=dev)
+    images, fim = Rasterize.apply(v, tex, vt, fi, ft, cfg)
+    if return_face_index:
+        return images, fim
+    return images
+
+
+def rasterize_silhouettes(vertices, faces, params: RasterizeParam, hyperparams: RasterizeHyperparam):
+    hyperparams.draw_rgb = False
+    hyperparams.draw_silhouettes = True
+    hyperparams.draw_depth = False
+    return rasterize_core(vertices, faces, params, hyperparams)[:, 0]
+
+
+def rasterize_rgba(vertices, faces, params: RasterizeParam, hyperparams: RasterizeHyperparam):
+    hyperparams.draw_rgb = True
+    hyperparams.draw_silhouettes = True
+    hyperparams.draw_depth = False
+    return rasterize_core(vertices=vertices, faces=faces, params=params, hyperparams=hyperparams)
+
+
+def rasterize_rgb(vertices, faces, params: RasterizeParam, hyperparams: RasterizeHyperparam):
+    hyperparams.draw_rgb = True
+    hyperparams.draw_silhouettes = False
+    hyperparams.draw_depth = False
+    return rasterize_core(vertices=vertices, faces=faces, params=params, hyperparams=hyperparams)
+
+
+def rasterize_depth(vertices, faces, params: RasterizeParam, hyperparams: RasterizeHyperparam):
+    hyperparams.draw_rgb = False
+    hyperparams.draw_silhouettes = False
+    hyperparams.draw_depth = True
+    return rasterize_core(vertices=vertices, faces=faces, params=params, hyperparams=hyperparams)[:, 0]

@@ -1,0 +1,258 @@
+"""Generate the golden vectors in tests/golden/*.npz by running the REFERENCE implementation.
+
+Run in the build container only (needs /root/reference):   python tests/golden/make_golden.py
+
+The reference Python package is imported through tests/golden/refimport.py (stubs for imageio,
+chainer and the CUDA extension; the extension's two kernels are served by the CPU oracle
+restatement).  Everything above the two kernels -- to_map, MaskForeground, the depth / coordinate /
+texture maps, Differentiation, flip and anti-aliasing, Renderer / look_at / perspective, load_obj --
+is the reference's own code, so these fixtures pin the oracle's Python restatement and the HIP
+path independently of them.  The face-index / weight kernels themselves are pinned by the
+reference's own data (tests/test_oracle_pins.py).
+
+Each fixture holds inputs and expected outputs only (no reference source).
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, REPO)
+import refimport  # noqa: E402
+from neural_renderer_v2_pytorch_amd import synthetic  # noqa: E402
+
+R = refimport.load()
+rast = sys.modules["nrt_ref.rasterize"]
+RP = sys.modules["nrt_ref.rasterize_param"]
+DATA = os.path.join(REPO, "tests", "data")
+TEAPOT = os.path.join(DATA, "teapot.obj")
+CAR = os.path.join(DATA, "4e49873292196f02574b5684eaec43e9", "model.obj")
+
+
+def save(name, **arrays):
+    out = {}
+    for k, v in arrays.items():
+        if torch.is_tensor(v):
+            v = v.detach().cpu().numpy()
+        out[k] = np.asarray(v)
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print("%-28s %8.1f KB  %s" % (name, os.path.getsize(path) / 1024, sorted(out)))
+
+
+def internals(proj, faces, S, near=0.1, far=100.0, draw_backside=True):
+    """face-index and weight maps through the reference's own rasterize.py:60-77 wrappers."""
+    hp = RP.RasterizeHyperparam(image_size=S, near=near, far=far, draw_backside=draw_backside)
+    fg = proj.detach()[:, torch.as_tensor(faces).long()]
+    fim = rast.compute_face_index_map(fg, hp)
+    w = rast.compute_weight_map(fg, fim)
+    return fim, w
+
+
+def flags_call(fn, proj, faces, params, hp):
+    leaf = proj.detach().clone().requires_grad_(True)
+    img = fn(leaf, torch.as_tensor(faces), params, hp)
+    return leaf, img
+
+
+def teapot_batch(slot=2, B=4):
+    v, f = R.load_obj.load_obj(TEAPOT)
+    vb = np.tile(v[None], (B, 1, 1)) * 0
+    vb[slot] = v
+    return vb.astype(np.float32), f
+
+
+def scene_square():
+    vertices = np.array([[0.1, 0.1, 1.], [-0.1, 0.1, 1.], [-0.1, -0.1, 1.], [0.1, -0.1, 1.]], 'float32')
+    faces = np.array([[0, 1, 2], [0, 2, 3]], 'int32')
+    ref = 1 - R.utils.imread(os.path.join(DATA, "gradient.png"))[:, :, 0]
+    ref = torch.as_tensor(ref)
+    v = torch.nn.Parameter(torch.as_tensor(vertices))
+    opt = torch.optim.Adam([v], lr=0.005)
+    first_grad = None
+    first_img = None
+    conv = -1
+    for i in range(350):
+        hp = RP.RasterizeHyperparam(image_size=256, anti_aliasing=False)
+        img = R.rasterize_silhouettes(v[None], torch.as_tensor(faces), RP.RasterizeParam(), hp)[0]
+        iou = torch.sum(img * ref) / torch.sum(img + ref - img * ref)
+        loss = 1 - iou
+        opt.zero_grad()
+        loss.backward()
+        if first_grad is None:
+            first_grad = v.grad.clone()
+            first_img = img.detach().clone()
+        opt.step()
+        if float(loss) < 0.01:
+            conv = i
+            break
+    fim, w = internals(torch.as_tensor(vertices)[None], faces, 256)
+    save("square_sil", vertices=vertices, faces=faces, fim=fim, weight_map=w, images=first_img[None],
+         iou_grad=first_grad, converge_step=np.int32(conv))
+
+
+def scene_teapot_sil():
+    vb, f = teapot_batch()
+    ren = R.Renderer()
+    ren.anti_aliasing = False
+    ren.viewpoints = R.utils.get_points_from_angles(2.732, 0, 0)
+    vt = torch.as_tensor(vb).requires_grad_(True)
+    proj = ren.transform_vertices(vt)
+    img = ren.render_silhouettes(vt, torch.as_tensor(f))
+    g = torch.as_tensor(np.random.RandomState(11).normal(size=img.shape).astype(np.float32))
+    img.backward(g)
+    leaf, img2 = flags_call(R.rasterize_silhouettes, proj, f, RP.RasterizeParam(),
+                            RP.RasterizeHyperparam(image_size=256, anti_aliasing=False))
+    img2.backward(g)
+    fim, w = internals(proj, f, 256)
+    save("teapot_sil", vertices=vb, faces=f, eye=np.asarray(ren.viewpoints, np.float32), proj=proj,
+         fim=fim, weight_map=w, images=img, grad_up=g, grad_vertices=vt.grad, grad_proj=leaf.grad)
+
+
+def scene_teapot_depth():
+    vb, f = teapot_batch()
+    ren = R.Renderer()
+    ren.anti_aliasing = False
+    ren.viewpoints = R.utils.get_points_from_angles(2, 30., 0)
+    vt = torch.as_tensor(vb)
+    proj = ren.transform_vertices(vt)
+    leaf, img = flags_call(R.rasterize_depth, proj, f, RP.RasterizeParam(),
+                           RP.RasterizeHyperparam(image_size=256, anti_aliasing=False))
+    g = torch.as_tensor(np.random.RandomState(12).normal(size=img.shape).astype(np.float32))
+    img.backward(g)
+    save("teapot_depth", vertices=vb, faces=f, eye=np.asarray(ren.viewpoints, np.float32), proj=proj,
+         images=img, grad_up=g, grad_proj=leaf.grad)
+
+
+def _textured(name, proj, f, vt_np, ft_np, tex_np, image_size, aa, draw_backside, fn, shared_tex, seed):
+    B = proj.shape[0]
+    tex_leaf = torch.as_tensor(tex_np).requires_grad_(True)
+    if shared_tex:
+        textures = tex_leaf[None].expand((B,) + tex_leaf.shape)
+        vts = torch.as_tensor(vt_np)[None].expand((B,) + vt_np.shape)
+    else:
+        textures = tex_leaf
+        vts = torch.as_tensor(vt_np)
+    params = RP.RasterizeParam(vertices_textures=vts, faces_textures=torch.as_tensor(ft_np), textures=textures)
+    hp = RP.RasterizeHyperparam(image_size=image_size, anti_aliasing=aa, draw_backside=draw_backside)
+    leaf, img = flags_call(fn, proj, f, params, hp)
+    g = torch.as_tensor(np.random.RandomState(seed).normal(size=img.shape).astype(np.float32))
+    img.backward(g)
+    S = image_size * (2 if aa else 1)
+    fim, w = internals(proj, f, S, draw_backside=draw_backside)
+    save(name, proj=proj, faces=f, vertices_textures=vt_np, faces_textures=ft_np, textures=tex_np,
+         shared_textures=np.int32(shared_tex), image_size=np.int32(image_size), anti_aliasing=np.int32(aa),
+         draw_backside=np.int32(draw_backside), fim=fim, weight_map=w, images=img, grad_up=g,
+         grad_proj=leaf.grad, grad_textures=tex_leaf.grad)
+
+
+def rasterize_all(v, f, params, hp):
+    hp.draw_rgb = hp.draw_silhouettes = hp.draw_depth = True
+    return rast.rasterize_core(v, f, params, hp)
+
+
+def scene_teapot_textured():
+    v, f = R.load_obj.load_obj(TEAPOT)
+    eyes = np.stack([R.utils.get_points_from_angles(2.732, 30, 30),
+                     R.utils.get_points_from_angles(2.732, -20, 135)]).astype(np.float32)
+    vb = torch.as_tensor(np.tile(v[None], (2, 1, 1)))
+    proj = R.perspective(R.look_at(vb, torch.as_tensor(eyes)))
+    vt, ft, tex = R.utils.create_textures(f.shape[0], texture_size=4)
+    tex = np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32)
+    _textured("teapot_rgbsd_aa", proj, f, vt, ft, tex, 64, True, True, rasterize_all, True, 21)
+    _textured("teapot_rgb_nobs", proj, f, vt, ft, tex, 96, False, False, R.rasterize_rgb, True, 22)
+    _textured("teapot_rgba_aa", proj, f, vt, ft, tex, 48, True, False, R.rasterize_rgba, True, 23)
+
+
+def scene_ico():
+    v, f = synthetic.icosphere(2)
+    B = 3
+    vb = synthetic.jittered(v, B)
+    eyes = synthetic.viewpoints(B)
+    # project per item (the reference look_at mis-crosses at batch size 3)
+    proj = torch.cat([R.perspective(R.look_at(torch.as_tensor(vb[b:b + 1]), torch.as_tensor(eyes[b:b + 1])))
+                      for b in range(B)], 0)
+    vt, ft, tex = R.utils.create_textures(f.shape[0], texture_size=4)
+    r = np.random.RandomState(4)
+    tex = r.uniform(0, 1, (B,) + tex.shape).astype(np.float32)
+    vt = np.tile(vt[None], (B, 1, 1))
+    _textured("ico_rgbsd_aa", proj, f, vt, ft, tex, 40, True, True, rasterize_all, False, 24)
+
+
+def scene_car():
+    ren = R.Renderer()
+    ren.draw_backside = False
+    ren.viewpoints = R.utils.get_points_from_angles(2.5, 10, -90)
+    v, f, vt, ft, tex = R.load_obj.load_obj(CAR, load_textures=True)
+    vv = torch.as_tensor(v[None])
+    img = ren.render(vv, torch.as_tensor(f), torch.as_tensor(vt[None]), torch.as_tensor(ft),
+                     torch.as_tensor(tex[None]))
+    proj = ren.transform_vertices(vv)
+    t = tex.astype(np.float64)
+    save("car1_rgba", vertices=v, faces=f, vertices_textures=vt, faces_textures=ft,
+         textures_shape=np.asarray(tex.shape), textures_sum=np.float64(t.sum()),
+         textures_sumsq=np.float64((t * t).sum()), eye=np.asarray(ren.viewpoints, np.float32), proj=proj,
+         images=img)
+
+
+def scene_diff_kat():
+    out = {}
+    for i, shape in enumerate([(3, 16, 16, 4), (2, 12, 20, 3), (1, 32, 32, 5)]):
+        r = np.random.RandomState(30 + i)
+        images = torch.as_tensor(r.normal(size=shape).astype(np.float32))
+        if i == 2:  # silhouette-like piecewise-constant images exercise the |R-L| < eps and max <= 0 rules
+            images = torch.as_tensor((r.uniform(size=shape) > 0.5).astype(np.float32))
+        coords = torch.zeros(shape[:3] + (2,), requires_grad=True)
+        g = torch.as_tensor(r.normal(size=shape).astype(np.float32))
+        y = R.differentiation.differentiation(images, coords)
+        y.backward(g)
+        out["images%d" % i] = images
+        out["grad%d" % i] = g
+        out["grad_xy%d" % i] = coords.grad
+    save("diff_kat", **out)
+
+
+def scene_edges():
+    """Adversarial face soups for the face-index kernel: pixel-aligned vertices (edge ties),
+    near-coplanar overlaps inside depth_min_delta (order dependence), degenerate and huge faces,
+    faces behind near / beyond far, NaN and inf coordinates."""
+    out = {}
+    for i, (B, F, S) in enumerate([(2, 300, 64), (1, 500, 50), (2, 64, 33)]):
+        r = np.random.RandomState(40 + i)
+        grid = (2 * r.randint(0, S, (B, F, 3, 2)) + 1 - S) / S              # pixel centres
+        jit = r.uniform(-1.3, 1.3, (B, F, 3, 2))
+        xy = np.where(r.uniform(size=(B, F, 1, 1)) < 0.5, grid, jit)
+        z = np.repeat(r.choice([1.0, 1.00003, 1.00006, 1.0001, 1.5, 2.0], (B, F, 1, 1)), 3, 2)
+        z = z + np.where(r.uniform(size=(B, F, 1, 1)) < 0.3, r.uniform(-0.2, 0.2, (B, F, 3, 1)), 0)
+        faces = np.concatenate([xy, z], -1).astype(np.float32)
+        faces[:, :8] = faces[:, :8] * 4                                       # huge faces
+        faces[:, 8:12, 2] = 0.05                                               # before near
+        faces[:, 12:16, 2] = 200.                                              # beyond far
+        faces[:, 16:20, 1] = faces[:, 16:20, 0]                                # degenerate
+        faces[:, 20, 0, 0] = np.nan
+        faces[:, 21, 1, 2] = np.nan
+        faces[:, 22, 2, 0] = np.inf
+        faces[:, 23, 0, 1] = -np.inf
+        for bs in (True, False):
+            fim = torch.as_tensor(refimport.oracle.face_index_map(faces, S, 0.1, 100.0, bs, 1e-4))
+            w = rast.compute_weight_map(torch.as_tensor(faces), fim)
+            # reference python path for the face-index wrapper, as a cross-check of the stub
+            hp = RP.RasterizeHyperparam(image_size=S, draw_backside=bs)
+            fim2 = rast.compute_face_index_map(torch.as_tensor(faces), hp)
+            assert torch.equal(fim, fim2)
+            out["faces%d" % i] = faces
+            out["fim%d_%d" % (i, bs)] = fim
+            out["weight%d_%d" % (i, bs)] = w
+    save("edges", **out)
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    todo = sys.argv[1:] or ["square", "teapot_sil", "teapot_depth", "teapot_textured", "ico", "car",
+                            "diff_kat", "edges"]
+    for name in todo:
+        globals()["scene_" + name]()

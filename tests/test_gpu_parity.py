@@ -1,0 +1,326 @@
+"""Parity of the HIP path (through the C ABI) with the reference, on the GPU.
+
+Golden vectors: tests/golden/*.npz, produced by the reference implementation itself
+(tests/golden/make_golden.py).  Large sizes are checked against the CPU oracle (oracle/).
+
+Tolerances (north star: face_index_map bit-exact; fp32 tolerance elsewhere):
+  * face_index_map, weight_map:   bit-exact
+  * images (rgb, depth, sil):     |d| <= 1e-5 + 1e-5 |ref|
+  * gradients (vertices, textures): |d| <= 1e-4 max|ref| + 1e-4 |ref| per element; float atomics
+    sum in a different order than the reference's index_put_ scatter.
+"""
+import numpy as np
+import pytest
+import torch
+
+import neural_renderer_v2_pytorch_amd as nr
+from neural_renderer_v2_pytorch_amd import rasterize as nrr
+from neural_renderer_v2_pytorch_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+IMG_RTOL = IMG_ATOL = 1e-5
+GRAD_TOL = 1e-4
+
+
+def close_images(a, b, what):
+    a = torch.as_tensor(a).detach().cpu().double()
+    b = torch.as_tensor(b).detach().cpu().double()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    err = (a - b).abs()
+    bad = err > IMG_ATOL + IMG_RTOL * b.abs()
+    assert not bad.any(), "%s: %d elements off, max |d| %g" % (what, int(bad.sum()), float(err.max()))
+
+
+def close_grads(a, b, what):
+    a = torch.as_tensor(a).detach().cpu().double()
+    b = torch.as_tensor(b).detach().cpu().double()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    scale = float(b.abs().max())
+    err = (a - b).abs()
+    bad = err > GRAD_TOL * scale + GRAD_TOL * b.abs()
+    assert not bad.any(), "%s: %d of %d elements off, max |d| %g (scale %g)" % (
+        what, int(bad.sum()), bad.numel(), float(err.max()), scale)
+
+
+def flags_of(name):
+    if "rgbsd" in name:
+        return dict(draw_rgb=True, draw_silhouettes=True, draw_depth=True)
+    if "rgba" in name:
+        return dict(draw_rgb=True, draw_silhouettes=True, draw_depth=False)
+    return dict(draw_rgb=True, draw_silhouettes=False, draw_depth=False)
+
+
+@pytest.mark.parametrize("name", ["teapot_rgbsd_aa", "teapot_rgb_nobs", "teapot_rgba_aa", "ico_rgbsd_aa"])
+def test_textured_scene(golden, dev, name):
+    d = golden(name)
+    B = d["proj"].shape[0]
+    proj = torch.as_tensor(d["proj"], device=dev).requires_grad_(True)
+    tex_leaf = torch.as_tensor(d["textures"], device=dev).requires_grad_(True)
+    if int(d["shared_textures"]):
+        tex = tex_leaf[None].expand(B, *tex_leaf.shape)
+        vt = torch.as_tensor(d["vertices_textures"], device=dev)[None].expand(B, -1, -1)
+    else:
+        tex = tex_leaf
+        vt = torch.as_tensor(d["vertices_textures"], device=dev)
+    params = nr.RasterizeParam(vertices_textures=vt, faces_textures=torch.as_tensor(d["faces_textures"], device=dev),
+                               textures=tex)
+    hp = nr.RasterizeHyperparam(image_size=int(d["image_size"]), anti_aliasing=bool(d["anti_aliasing"]),
+                                draw_backside=bool(d["draw_backside"]), **flags_of(name))
+    img, fim = nrr.rasterize_core(proj, torch.as_tensor(d["faces"], device=dev), params, hp, return_face_index=True)
+    assert torch.equal(fim.cpu(), torch.as_tensor(d["fim"])), "face_index_map not bit-exact"
+    close_images(img, d["images"], name + " images")
+    img.backward(torch.as_tensor(d["grad_up"], device=dev))
+    close_grads(proj.grad, d["grad_proj"], name + " grad vertices")
+    close_grads(tex_leaf.grad, d["grad_textures"], name + " grad textures")
+
+
+def test_wrappers_match_core(golden, dev):
+    """rasterize_rgba / rasterize_rgb set the draw flags on the passed hyperparams (rasterize.py:341-356)."""
+    d = golden("teapot_rgba_aa")
+    B = d["proj"].shape[0]
+    proj = torch.as_tensor(d["proj"], device=dev)
+    tex = torch.as_tensor(d["textures"], device=dev)[None].expand(B, -1, -1, -1)
+    vt = torch.as_tensor(d["vertices_textures"], device=dev)[None].expand(B, -1, -1)
+    params = nr.RasterizeParam(vertices_textures=vt, faces_textures=torch.as_tensor(d["faces_textures"], device=dev),
+                               textures=tex)
+    hp = nr.RasterizeHyperparam(image_size=int(d["image_size"]), anti_aliasing=True, draw_backside=False)
+    img = nr.rasterize_rgba(proj, torch.as_tensor(d["faces"], device=dev), params, hp)
+    assert (hp.draw_rgb, hp.draw_silhouettes, hp.draw_depth) == (True, True, False)
+    assert hp.image_size == int(d["image_size"])
+    close_images(img, d["images"], "rasterize_rgba")
+
+
+def test_silhouettes_teapot(golden, dev):
+    d = golden("teapot_sil")
+    proj = torch.as_tensor(d["proj"], device=dev).requires_grad_(True)
+    hp = nr.RasterizeHyperparam(image_size=256, anti_aliasing=False)
+    img = nr.rasterize_silhouettes(proj, torch.as_tensor(d["faces"]), nr.RasterizeParam(), hp)
+    assert torch.equal(img.detach().cpu(), torch.as_tensor(d["images"]))
+    img.backward(torch.as_tensor(d["grad_up"], device=dev))
+    close_grads(proj.grad, d["grad_proj"], "teapot silhouettes grad")
+    fim = nrr.compute_face_index_map(torch.as_tensor(d["proj"], device=dev)[:, torch.as_tensor(d["faces"]).long()],
+                                     nr.RasterizeHyperparam(image_size=256))
+    assert torch.equal(fim.cpu(), torch.as_tensor(d["fim"]))
+    w = nrr.compute_weight_map(torch.as_tensor(d["proj"], device=dev)[:, torch.as_tensor(d["faces"]).long()], fim)
+    assert torch.equal(w.cpu(), torch.as_tensor(d["weight_map"])), "weight_map not bit-exact"
+
+
+def test_renderer_silhouettes_teapot(golden, dev):
+    """Renderer path (look_at + perspective on the GPU, then rasterize): the camera transform runs on
+    the GPU's BLAS, so projected vertices may differ from the CPU reference in the last ulp."""
+    d = golden("teapot_sil")
+    ren = nr.Renderer()
+    ren.anti_aliasing = False
+    ren.viewpoints = nr.get_points_from_angles(2.732, 0, 0)
+    v = torch.as_tensor(d["vertices"], device=dev).requires_grad_(True)
+    img = ren.render_silhouettes(v, torch.as_tensor(d["faces"], device=dev))
+    diff = (img.detach().cpu() != torch.as_tensor(d["images"])).float().mean().item()
+    assert diff < 1e-3, diff
+    img.backward(torch.as_tensor(d["grad_up"], device=dev))
+    g, ref = v.grad.cpu()[2], torch.as_tensor(d["grad_vertices"])[2]
+    assert float((g - ref).abs().sum() / ref.abs().sum()) < 2e-2
+
+
+def test_depth_teapot(golden, dev):
+    d = golden("teapot_depth")
+    proj = torch.as_tensor(d["proj"], device=dev).requires_grad_(True)
+    hp = nr.RasterizeHyperparam(image_size=256, anti_aliasing=False)
+    img = nr.rasterize_depth(proj, torch.as_tensor(d["faces"], device=dev), nr.RasterizeParam(), hp)
+    close_images(img, d["images"], "depth")
+    img.backward(torch.as_tensor(d["grad_up"], device=dev))
+    close_grads(proj.grad, d["grad_proj"], "depth grad")
+
+
+def test_square_first_step_gradient(golden, dev):
+    """test_backward_case1's scene: the IoU-loss gradient of the first step (reference: +-0.0617 in x/y,
+    exactly 0 in z)."""
+    d = golden("square_sil")
+    from PIL import Image
+    import os
+    ref = 1 - np.asarray(Image.open(os.path.join(os.path.dirname(__file__), "data", "gradient.png")),
+                         np.float32)[:, :, 0] / 255.
+    ref = torch.as_tensor(ref, device=dev)
+    v = torch.as_tensor(d["vertices"], device=dev).requires_grad_(True)
+    hp = nr.RasterizeHyperparam(image_size=256, anti_aliasing=False)
+    img = nr.rasterize_silhouettes(v[None], torch.as_tensor(d["faces"]), nr.RasterizeParam(), hp)[0]
+    assert torch.equal(img.detach().cpu(), torch.as_tensor(d["images"][0]))
+    iou = torch.sum(img * ref) / torch.sum(img + ref - img * ref)
+    (1 - iou).backward()
+    close_grads(v.grad, d["iou_grad"], "square iou grad")
+    assert torch.all(v.grad[:, 2] == 0)
+
+
+def test_backward_case1_convergence(dev):
+    """tests_torch/test_rasterize.py:205-249: Adam(lr=0.005) on a 2-triangle square reaches
+    1 - IoU < 0.01 within 350 steps (reference on CPU oracle: step 221)."""
+    import os
+    from PIL import Image
+    vertices = np.array([[0.1, 0.1, 1.], [-0.1, 0.1, 1.], [-0.1, -0.1, 1.], [0.1, -0.1, 1.]], 'float32')
+    faces = torch.as_tensor(np.array([[0, 1, 2], [0, 2, 3]], 'int32'), device=dev)
+    ref = 1 - np.asarray(Image.open(os.path.join(os.path.dirname(__file__), "data", "gradient.png")),
+                         np.float32)[:, :, 0] / 255.
+    ref = torch.as_tensor(ref, device=dev)
+    v = torch.nn.Parameter(torch.as_tensor(vertices, device=dev))
+    opt = torch.optim.Adam([v], lr=0.005)
+    for i in range(350):
+        hp = nr.RasterizeHyperparam(image_size=256, anti_aliasing=False)
+        img = nr.rasterize_silhouettes(v[None], faces, nr.RasterizeParam(), hp)[0]
+        loss = 1 - torch.sum(img * ref) / torch.sum(img + ref - img * ref)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        if float(loss) < 0.01:
+            assert abs(i - 221) <= 10, i
+            return
+    raise AssertionError("did not converge")
+
+
+def test_car_rgba(golden, dev):
+    """test_forward_case2 / test_save_obj scene (car 4e4987...): load_obj + Renderer.render, rgba."""
+    import os
+    d = golden("car1_rgba")
+    obj = os.path.join(os.path.dirname(__file__), "data", "4e49873292196f02574b5684eaec43e9", "model.obj")
+    v, f, vt, ft, tex = nr.load_obj(obj, load_textures=True)
+    assert np.array_equal(v, d["vertices"]) and np.array_equal(f, d["faces"])
+    assert np.array_equal(vt, d["vertices_textures"]) and np.array_equal(ft, d["faces_textures"])
+    assert list(tex.shape) == list(d["textures_shape"])
+    assert abs(tex.astype(np.float64).sum() - float(d["textures_sum"])) < 1e-6 * float(d["textures_sum"])
+    ren = nr.Renderer()
+    ren.draw_backside = False
+    ren.viewpoints = nr.get_points_from_angles(2.5, 10, -90)
+    proj = torch.as_tensor(d["proj"], device=dev)
+    hp = nr.RasterizeHyperparam(image_size=256, draw_backside=False)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None],
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=torch.as_tensor(tex, device=dev)[None])
+    img = nr.rasterize_rgba(proj, torch.as_tensor(f, device=dev), params, hp)
+    close_images(img, d["images"], "car rgba")
+    # the reference's own golden PNG (tests_torch/data/4e49...png): alpha channel
+    from PIL import Image
+    png = np.asarray(Image.open(os.path.join(os.path.dirname(__file__), "data",
+                                             "4e49873292196f02574b5684eaec43e9.png")), np.float32) / 255.
+    alpha = img[0, 3].cpu().numpy()
+    assert np.abs(alpha - png[:, :, 3]).mean() < 1e-4
+
+
+def test_differentiation_golden(golden, dev):
+    d = golden("diff_kat")
+    for i in range(3):
+        images = torch.as_tensor(d["images%d" % i], device=dev)
+        coords = torch.zeros(images.shape[:3] + (2,), device=dev, requires_grad=True)
+        y = nr.differentiation(images, coords)
+        y.backward(torch.as_tensor(d["grad%d" % i], device=dev))
+        close_images(coords.grad, d["grad_xy%d" % i], "differentiation %d" % i)
+
+
+def test_differentiation_reference_procedure(dev):
+    """tests_torch/test_differentiation.py:10-65, verbatim procedure on the GPU implementation."""
+    r = np.random.RandomState(0)
+    images = torch.as_tensor(r.normal(size=(10, 32, 32, 3)).astype('float32'), device=dev)
+    x = np.tile(np.arange(32).astype('float32')[None, None, :, None], (10, 32, 1, 1))
+    y = np.tile(np.arange(32).astype('float32')[None, :, None, None], (10, 1, 32, 1))
+    coordinates = ((np.concatenate((x, y), axis=-1) / 31) * 2 - 1) * 31. / 32.
+    noise = torch.as_tensor(r.normal(size=(10, 32, 32, 3)).astype('float32'), device=dev)
+    step = 2 / 32.
+    coordinates = torch.tensor(coordinates, device=dev, requires_grad=True)
+    torch.sum(nr.differentiation(images, coordinates) * noise).backward()
+    g = coordinates.grad
+    for _ in range(100):
+        yi, xi = r.randint(1, 31), r.randint(1, 31)
+        pairs = []
+        for axis in (1, 0):
+            for sgn in (1, -1):
+                im = images.clone()
+                if axis == 1:
+                    im[:, yi - sgn, xi] = images[:, yi, xi]
+                    im[:, yi, xi] = images[:, yi + sgn, xi]
+                else:
+                    im[:, yi, xi - sgn] = images[:, yi, xi]
+                    im[:, yi, xi] = images[:, yi, xi + sgn]
+                gg = ((im - images) * noise).sum((1, 2, 3)) / step
+                pairs.append(torch.min(gg, torch.zeros_like(gg)))
+        gy = torch.max(pairs[0].abs(), pairs[1].abs())
+        gx = torch.max(pairs[2].abs(), pairs[3].abs())
+        assert torch.allclose(gy, g[:, yi, xi, 1].abs().to(gy.dtype), rtol=1e-4, atol=0)
+        assert torch.allclose(gx, g[:, yi, xi, 0].abs().to(gx.dtype), rtol=1e-4, atol=0)
+
+
+def test_edges_face_index(golden, dev):
+    d = golden("edges")
+    for i in range(3):
+        faces = torch.as_tensor(d["faces%d" % i], device=dev)
+        S = d["fim%d_1" % i].shape[1]
+        for bs in (0, 1):
+            hp = nr.RasterizeHyperparam(image_size=S, draw_backside=bool(bs))
+            fim = nrr.compute_face_index_map(faces, hp)
+            ref = torch.as_tensor(d["fim%d_%d" % (i, bs)])
+            assert torch.equal(fim.cpu(), ref), "edges %d backside %d: %d px differ" % (
+                i, bs, int((fim.cpu() != ref).sum()))
+            w = nrr.compute_weight_map(faces, fim)
+            np.testing.assert_array_equal(w.cpu().numpy(), d["weight%d_%d" % (i, bs)])
+
+
+def _ico_batch(level, B, dev):
+    v, f = synthetic.icosphere(level)
+    vb = torch.as_tensor(synthetic.jittered(v, B))
+    proj = synthetic.project(vb, torch.as_tensor(synthetic.viewpoints(B)))
+    return proj, f
+
+
+@pytest.mark.parametrize("S,level,B", [(512, 4, 2), (1000, 3, 1), (130, 4, 3)])
+def test_face_index_large_vs_oracle(oracle_mod, dev, S, level, B):
+    """Headline-size face-index map (ico-sphere 5120 faces, 512^2 internal) bit-exact against the
+    brute-force CPU oracle; plus a non-multiple-of-tile size."""
+    proj, f = _ico_batch(level, B, dev)
+    fg = proj[:, torch.as_tensor(f).long()].contiguous()
+    fim = nrr.compute_face_index_map(fg.to(dev), nr.RasterizeHyperparam(image_size=S))
+    ref = oracle_mod.face_index_map(fg, S)
+    assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
+
+
+def test_headline_properties(dev):
+    """Full headline config (B=64, 256^2 AA, ico 5120, rgb+sil+depth): size-independent properties."""
+    B = 64
+    proj, f = _ico_batch(4, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.rand(tex.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(3), requires_grad=True)
+    pv = proj.to(dev).requires_grad_(True)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+    img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
+                                  return_face_index=True)
+    assert img.shape == (B, 5, 256, 256)
+    sil = img[:, 3]
+    # silhouette = 2x2 average of the flipped (fim >= 0) mask
+    m = (fim >= 0).float().flip(1, 2)
+    m = (m[:, 0::2, 0::2] + m[:, 1::2, 0::2] + m[:, 0::2, 1::2] + m[:, 1::2, 1::2]) / 4
+    assert torch.equal(sil, m)
+    assert torch.isfinite(img).all()
+    assert float(img[:, :3].min()) >= 0 and float(img[:, :3].max()) <= 1 + 1e-6
+    # item independence: rendering item 5 alone gives the same item-5 output
+    params1 = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None],
+                                faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None])
+    img1 = nrr.rasterize_core(pv[5:6].detach(), torch.as_tensor(f, device=dev), params1, nr.RasterizeHyperparam())
+    assert torch.equal(img1[0], img[5].detach())
+    g = torch.randn_like(img)
+    img.backward(g)
+    assert torch.isfinite(pv.grad).all() and torch.isfinite(tex.grad).all()
+    # linearity of the backward in the upstream gradient
+    pv2 = proj.to(dev).requires_grad_(True)
+    img2 = nrr.rasterize_core(pv2, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam())
+    img2.backward(2 * g)
+    assert float((pv2.grad - 2 * pv.grad).abs().max()) <= 1e-3 * float(pv.grad.abs().max())
+
+
+def test_empty_and_degenerate(dev):
+    hp = nr.RasterizeHyperparam(image_size=16)
+    v = torch.zeros((0, 3, 3), device=dev)
+    f = torch.as_tensor([[0, 1, 2]], device=dev)
+    out = nr.rasterize_silhouettes(v, f, nr.RasterizeParam(), hp)
+    assert out.shape == (0, 16, 16)
+    v = torch.rand((2, 5, 3), device=dev)
+    out = nr.rasterize_depth(v, torch.zeros((0, 3), dtype=torch.int32), nr.RasterizeParam(),
+                             nr.RasterizeHyperparam(image_size=10, anti_aliasing=False))
+    assert out.shape == (2, 10, 10) and float(out.abs().max()) == 0
+    with pytest.raises(IndexError):
+        nr.rasterize_silhouettes(v, torch.as_tensor([[0, 1, 7]]), nr.RasterizeParam(), hp)

@@ -1,0 +1,128 @@
+"""Host-side logic and the C ABI library (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import neural_renderer_v2_pytorch_amd as nr
+from neural_renderer_v2_pytorch_amd import _lib, synthetic
+from conftest import DATA, ROOT
+
+
+def test_look_at_kat():
+    """tests_torch/test_look_at.py:10-26."""
+    vertices = torch.as_tensor(np.array([1, 0, 0], 'float32'))[None, None, :]
+    cases = [([1, 0, 1], [-np.sqrt(2) / 2, 0, np.sqrt(2) / 2]), ([0, 0, -10], [1, 0, 10]),
+             ([-1, 1, 0], [0, np.sqrt(2) / 2, 3. / 2. * np.sqrt(2)])]
+    for e, a in cases:
+        out = nr.look_at(vertices, torch.as_tensor(np.array(e, 'float32')))
+        np.testing.assert_allclose(out.flatten().numpy(), np.array(a), rtol=1e-6, atol=1e-6)
+
+
+def test_perspective_kat():
+    """tests_torch/test_perspective.py:10-16."""
+    v = torch.as_tensor(np.array([1, 2, 10], 'float32'))[None, None, :]
+    np.testing.assert_allclose(nr.perspective(v).flatten().numpy(),
+                               np.asarray([np.sqrt(3) / 10, 2 * np.sqrt(3) / 10, 10], np.float32), rtol=1e-5)
+
+
+def test_look_at_batch3_is_per_item():
+    """The reference's dim-less torch.cross mixes items at batch size 3; ours is per item."""
+    v = torch.randn(3, 7, 3)
+    eyes = torch.as_tensor(synthetic.viewpoints(3))
+    batched = nr.look_at(v, eyes)
+    single = torch.cat([nr.look_at(v[i:i + 1], eyes[i:i + 1]) for i in range(3)])
+    assert torch.allclose(batched, single, atol=1e-6)
+
+
+def test_renderer_transform_matches_golden(golden):
+    d = golden("teapot_sil")
+    ren = nr.Renderer()
+    ren.viewpoints = nr.get_points_from_angles(2.732, 0, 0)
+    proj = ren.transform_vertices(torch.as_tensor(d["vertices"]))
+    np.testing.assert_allclose(proj.numpy(), d["proj"], rtol=1e-6, atol=1e-6)
+
+
+def test_load_obj_car_matches_reference(golden):
+    d = golden("car1_rgba")
+    v, f, vt, ft, tex = nr.load_obj(os.path.join(DATA, "4e49873292196f02574b5684eaec43e9", "model.obj"),
+                                    load_textures=True)
+    assert np.array_equal(v, d["vertices"]) and np.array_equal(f, d["faces"])
+    assert np.array_equal(vt, d["vertices_textures"]) and np.array_equal(ft, d["faces_textures"])
+    t = tex.astype(np.float64)
+    assert list(tex.shape) == list(d["textures_shape"])
+    assert abs(t.sum() - float(d["textures_sum"])) <= 1e-9 * float(d["textures_sum"])
+    assert abs((t * t).sum() - float(d["textures_sumsq"])) <= 1e-9 * float(d["textures_sumsq"])
+
+
+def test_load_obj_teapot(golden):
+    v, f = nr.load_obj(os.path.join(DATA, "teapot.obj"))
+    d = golden("teapot_sil")
+    assert np.array_equal(v, d["vertices"][2]) and np.array_equal(f, d["faces"])
+
+
+def test_save_load_roundtrip(tmp_path):
+    v, f, vt, ft, tex = nr.load_obj(os.path.join(DATA, "4e49873292196f02574b5684eaec43e9", "model.obj"),
+                                    load_textures=True)
+    path = str(tmp_path / "m.obj")
+    nr.save_obj(path, v, f, vt, ft, tex)
+    v2, f2, vt2, ft2, tex2 = nr.load_obj(path, load_textures=True, normalization=False)
+    assert np.allclose(v2, v, atol=1e-6) and np.array_equal(f2, f) and np.array_equal(ft2, ft)
+    assert tex2.shape == tex.shape and np.abs(tex2 - tex).max() <= 1 / 255. + 1e-6
+
+
+def test_create_textures_layout():
+    vt, ft, tex = nr.create_textures(5120, texture_size=4)
+    assert tex.shape == (3, 288, 288) and vt.shape == (5120 * 3, 2) and ft.shape == (5120, 3)
+    assert vt.max() == 287 and vt.min() == 0
+
+
+def test_synthetic_meshes():
+    v, f = synthetic.icosphere(4)
+    assert v.shape == (2562, 3) and f.shape == (5120, 3)
+    v, f = synthetic.torus()
+    assert v.shape == (25000, 3) and f.shape == (50000, 3)
+    assert f.min() == 0 and f.max() == 24999
+
+
+def test_library_exports_every_header_symbol():
+    """The C-ABI library loads and exports exactly what include/nr_raster.h declares."""
+    header = open(os.path.join(ROOT, "include", "nr_raster.h")).read()
+    declared = set(re.findall(r"^\s*(?:NR_API\s+)?(?:const\s+)?\w+\s*\*?\s*(nr_\w+)\s*\(", header, re.M))
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert _lib.lib().nr_version() == 1
+    assert _lib.lib().nr_num_channels(7) == 5 and _lib.lib().nr_num_channels(2) == 1
+    assert _lib.lib().nr_workspace_bytes(64, 5120, 512) >= 64 * 5120 * 8 + 64 * 64 * 160 * 4
+
+
+def test_abi_rejects_bad_arguments():
+    """Error behaviour without touching the GPU: argument validation runs before any launch."""
+    L = _lib.lib()
+    st = L.nr_face_index_map_forward_safe(None, None, 1, 10, 0, 0.1, 100., 1, 1e-8, 1e-4, None, 0, None)
+    assert st == 1 and b"bad sizes" in L.nr_last_error()
+    a = _lib.NrRasterArgs()
+    a.batch_size, a.num_faces, a.num_vertices, a.image_size, a.draw_flags = 1, 1, 3, 8, 0
+    assert L.nr_rasterize_forward(ctypes.byref(a), None, None) == 1
+    assert b"nothing to draw" in L.nr_last_error()
+
+
+def test_no_cpu_fallback():
+    v = torch.rand(1, 3, 3)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        nr.rasterize_silhouettes(v, torch.as_tensor([[0, 1, 2]]), nr.RasterizeParam(), nr.RasterizeHyperparam())
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "neural_renderer_v2_pytorch_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".hip", ".h", ".cpp")):
+                src = open(os.path.join(dirpath, fn)).read()
+                assert not re.search(r"^\s*(import|from)\s+oracle", src, re.M), fn
+                assert "libnr_oracle" not in src, fn

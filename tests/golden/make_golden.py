@@ -71,7 +71,7 @@ def scene_square():
     faces = np.array([[0, 1, 2], [0, 2, 3]], 'int32')
     ref = 1 - R.utils.imread(os.path.join(DATA, "gradient.png"))[:, :, 0]
     ref = torch.as_tensor(ref)
-    v = torch.nn.Parameter(torch.as_tensor(vertices))
+    v = torch.nn.Parameter(torch.tensor(vertices))  # a copy: Adam updates v in place
     opt = torch.optim.Adam([v], lr=0.005)
     first_grad = None
     first_img = None

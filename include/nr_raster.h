@@ -109,8 +109,12 @@ typedef struct NrRasterArgs {
     float* face_records;     /* [B, F, 9]: gathered faces (rasterize.py:232) */
     float* face_uv;          /* [Buv, F, 6] with Buv = (vt_batch_stride ? B : 1); only with RGB */
     int32_t* face_index;     /* [B, S, S] */
-    void* workspace;
+    void* workspace;         /* forward scratch, nr_workspace_bytes(B, F, S) */
     size_t workspace_bytes;
+    /* backward only: CSR adjacency vertex -> face corners, built once per faces tensor.
+     * vertex_faces[vertex_offsets[v] .. vertex_offsets[v+1]) lists 3 f + k for every faces[f, k] == v. */
+    const int32_t* vertex_offsets; /* [V + 1] */
+    const int32_t* vertex_faces;   /* [3 F] */
 } NrRasterArgs;
 
 /* Channels in output order: rgb (3), silhouettes (1), depth (1) -- those enabled by draw_flags. */
@@ -119,11 +123,17 @@ NR_API int nr_num_channels(int draw_flags);
 /* rasterize.py:194-329 (without lights / backgrounds): images [B, C, s, s] contiguous. */
 NR_API int nr_rasterize_forward(const NrRasterArgs* args, float* images, void* stream);
 
-/* Backward of nr_rasterize_forward for upstream grad_images [B, C, s, s] (contiguous).
- * Accumulates (+=) into grad_vertices [B, V, 3] and, with NR_DRAW_RGB and grad_textures != NULL,
- * grad_textures [Bt, 3, H, W] contiguous, Bt = (tex_stride_b ? B : 1).  Callers zero them first. */
+/* Scratch bytes of nr_rasterize_backward: per-face gradient records [B, F, 9] and the texture
+ * gradient accumulator [texture_items, H*W rounded up to 4, 4]. */
+NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int texture_items, int tex_height,
+                                          int tex_width);
+
+/* Backward of nr_rasterize_forward for upstream grad_images [B, C, s, s] (contiguous), given the
+ * state the forward saved in `args`.  Writes grad_vertices [B, V, 3] and, with NR_DRAW_RGB and
+ * grad_textures != NULL, grad_textures [Bt, 3, H, W] contiguous with Bt = (tex_stride_b ? B : 1)
+ * (the batch total when the textures are shared).  Needs args->vertex_offsets/vertex_faces. */
 NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
-                          float* grad_textures, void* stream);
+                                 float* grad_textures, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

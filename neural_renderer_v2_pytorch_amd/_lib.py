@@ -10,7 +10,8 @@ import os
 import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "libnr_raster.so")
+# NR_LIB_PATH: developer override used by the timing-variant scripts in tools/
+LIB_PATH = os.environ.get("NR_LIB_PATH") or os.path.join(LIB_DIR, "libnr_raster.so")
 
 NR_DRAW_RGB = 1
 NR_DRAW_SILHOUETTES = 2
@@ -21,6 +22,7 @@ EXPORTS = [
     "nr_last_error", "nr_version", "nr_workspace_bytes", "nr_face_index_map_forward_safe",
     "nr_compute_weight_map", "nr_mask_foreground_forward", "nr_mask_foreground_backward",
     "nr_differentiation_backward", "nr_num_channels", "nr_rasterize_forward", "nr_rasterize_backward",
+    "nr_backward_workspace_bytes",
 ]
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
@@ -38,6 +40,7 @@ class NrRasterArgs(ctypes.Structure):
         ("tex_height", c_int), ("tex_width", c_int),
         ("face_records", c_void_p), ("face_uv", c_void_p), ("face_index", c_void_p),
         ("workspace", c_void_p), ("workspace_bytes", c_size_t),
+        ("vertex_offsets", c_void_p), ("vertex_faces", c_void_p),
     ]
 
 
@@ -66,9 +69,12 @@ def lib():
     L.nr_mask_foreground_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]
     L.nr_differentiation_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
     L.nr_rasterize_forward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p]
-    L.nr_rasterize_backward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p]
+    L.nr_rasterize_backward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_size_t, c_void_p]
+    L.nr_backward_workspace_bytes.restype = c_size_t
+    L.nr_backward_workspace_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int]
     for name in EXPORTS:
-        if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels"):
+        if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels", "nr_backward_workspace_bytes"):
             getattr(L, name).restype = c_int
     _lib = L
     return L

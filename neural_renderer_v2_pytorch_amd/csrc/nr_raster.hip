@@ -362,9 +362,19 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_raster_fwd: per 32x8 tile.  LDS face record (8 x float4):
-//   0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
-//   4: z2 A B C            | 5: D E F nD      | 6: nF nB k0 k1 | 7: k2 - - -
+// k_raster_fwd: per 32x8 tile.
+//   face list: the coarse bin's bitmask words are expanded (block scan over popcounts) into an
+//   ordered candidate list in LDS; candidates are then tested against the tile 256 at a time (one
+//   bbox load per thread) and the survivors appended in order (ballot + popcount prefix) to the
+//   LDS face stage, which is rasterised whenever it would overflow -- so every pixel sees its
+//   faces in ascending index order, as the reference's sequential loop does.
+//   LDS face record (7 x float4):
+//     0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
+//     4: z2 A=x1-x0 B=y1-y0 C=x2-x1 | 5: D=y2-y1 E=x0-x2 F=y0-y2 k0 | 6: k1 k2 - -
+//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
+constexpr int CAND = 1024;
+constexpr int FREC = 7;
+
 struct FwdOut {
     float* images;   // [B, C, s, s] (FUSED only)
     int32_t* fim;    // [B, S, S]
@@ -377,12 +387,76 @@ __device__ __forceinline__ void pixel_of(int t, int& lx, int& ly) {
     ly = (w >> 1) * 4 + (l >> 4);
 }
 
+struct PixState {
+    float depth_min;
+    int best;
+    Face bf;
+};
+
+// the reference's per-face test sequence (.cu:94-148) over n staged faces
+__device__ __forceinline__ void raster_staged(const float4 (*s_face)[FREC], int n, float xp, float yp, int wx0, int wx1,
+                                              int wy0, int wy1, float near, float far, float delta, PixState& ps) {
+    for (int i = 0; i < n; i++) {
+        const float4 q1 = s_face[i][1];
+        const int bx = __float_as_int(q1.x), by = __float_as_int(q1.y);
+        // wave-uniform skip: face bbox misses this wave's 16x4 pixels
+        if (range_lo(bx) > wx1 || range_hi(bx) < wx0 || range_lo(by) > wy1 || range_hi(by) < wy0) continue;
+        const float4 q0 = s_face[i][0];
+        // .cu:94-97 (min/max form, exact for non-NaN faces)
+        if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) continue;
+        const float4 q2 = s_face[i][2], q3 = s_face[i][3], q4 = s_face[i][4], q5 = s_face[i][5];
+        const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
+        // .cu:107-116
+        const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
+        const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
+        if (c1 * c2 < 0) continue;
+        const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
+        if (c2 * c3 < 0) continue;
+        // .cu:124-126
+        if (ps.depth_min < q1.z) continue;
+        const float4 q6 = s_face[i][6];
+        const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
+        // .cu:130-139
+        float w0 = (yp * q4.w - xp * q5.x) + q5.w;
+        float w1 = (yp * q5.y - xp * q5.z) + q6.x;
+        float w2 = (yp * q4.y - xp * q4.z) + q6.y;
+        const float ws = w0 + w1 + w2;
+        w0 /= ws;
+        w1 /= ws;
+        w2 /= ws;
+        const float zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
+        if (zp <= near || far <= zp) continue;
+        if (zp <= ps.depth_min - delta) {  // .cu:145-148
+            ps.depth_min = zp;
+            ps.best = __float_as_int(q1.w);
+            ps.bf.x0 = x0; ps.bf.y0 = y0; ps.bf.z0 = z0;
+            ps.bf.x1 = x1; ps.bf.y1 = y1; ps.bf.z1 = z1;
+            ps.bf.x2 = x2; ps.bf.y2 = y2; ps.bf.z2 = z2;
+        }
+    }
+}
+
+__device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f, int2 bb) {
+    const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
+    const float x2 = c[6], y2 = c[7], z2 = c[8];
+    e[0] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
+                       fmaxf(fmaxf(y0, y1), y2));
+    e[1] = make_float4(__int_as_float(bb.x), __int_as_float(bb.y), fminf(fminf(z0, z1), z2), __int_as_float(f));
+    e[2] = make_float4(x0, y0, x1, y1);
+    e[3] = make_float4(x2, y2, z0, z1);
+    e[4] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
+    e[5] = make_float4(y2 - y1, x0 - x2, y0 - y2, x1 * y2 - x2 * y1);
+    e[6] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, 0.f, 0.f);
+}
+
 template <bool FUSED>
 __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, const int2* __restrict__ bbox,
                                                   const uint32_t* __restrict__ mask, int F, Geom g, float near,
                                                   float far, float delta, Shade sh, int aa, FwdOut out) {
-    __shared__ float4 s_face[CAP][8];
+    __shared__ float4 s_face[CAP][FREC];
+    __shared__ int s_cand[CAND];
     __shared__ int s_scan[4];
+    __shared__ int s_wcnt[4];
     __shared__ float s_chan[FUSED ? MAXC : 1][NT];
 
     const int b = blockIdx.y;
@@ -390,113 +464,83 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
     const int tx0 = (blockIdx.x % g.tiles_x) * TW;
     const int ty0 = (blockIdx.x / g.tiles_x) * TH;
     const int t = threadIdx.x;
+    const int lane = t & 63, wid = t >> 6;
     int lx, ly;
     pixel_of(t, lx, ly);
     const int px = tx0 + lx, py = ty0 + ly;
     const float xp = pix_center(px, S);
     const float yp = pix_center(py, S);
     // this wave's pixel rectangle, for the wave-uniform face skip
-    const int wave = t >> 6;
-    const int wx0 = tx0 + (wave & 1) * 16, wy0 = ty0 + (wave >> 1) * 4;
+    const int wx0 = tx0 + (wid & 1) * 16, wy0 = ty0 + (wid >> 1) * 4;
     const int wx1 = wx0 + 15, wy1 = wy0 + 3;
     const int tx1 = tx0 + TW - 1, ty1 = ty0 + TH - 1;
 
-    float depth_min = far;
-    int best = -1;
-    Face bf = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    PixState ps;
+    ps.depth_min = far;
+    ps.best = -1;
+    ps.bf = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
     const int bin = (ty0 / COARSE) * g.nbx + (tx0 / COARSE);
     const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
     const int2* bbb = bbox + (long long)b * F;
     const float* frb = face_records + (long long)b * F * 9;
+    int nstaged = 0;
 
     for (int wbase = 0; wbase < g.nwords; wbase += NT) {
         const int w = wbase + t;
-        uint32_t bits = (w < g.nwords) ? words[w] : 0u;
-        uint32_t keep = 0;
-        for (uint32_t m = bits; m; m &= m - 1) {
-            const int j = __builtin_ctz(m);
-            const int2 bb = bbb[w * 32 + j];
-            if (range_lo(bb.x) <= tx1 && range_hi(bb.x) >= tx0 && range_lo(bb.y) <= ty1 && range_hi(bb.y) >= ty0)
-                keep |= 1u << j;
-        }
+        const uint32_t bits = (w < g.nwords) ? words[w] : 0u;
         int total;
-        const int off = block_scan(__builtin_popcount(keep), total, s_scan);
-        for (int base = 0; base < total; base += CAP) {
-            // stage faces ranked [base, base + CAP) in ascending face order
+        const int off = block_scan(__builtin_popcount(bits), total, s_scan);
+        for (int cbase = 0; cbase < total; cbase += CAND) {
+            // expand my word's set bits into the ordered candidate list
             int r = off;
-            for (uint32_t m = keep; m; m &= m - 1, r++) {
-                if (r < base) continue;
-                if (r >= base + CAP) break;
-                const int j = __builtin_ctz(m);
-                const int f = w * 32 + j;
-                const float* c = frb + (long long)f * 9;
-                const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
-                const float x2 = c[6], y2 = c[7], z2 = c[8];
-                const int2 bb = bbb[f];
-                float4* e = s_face[r - base];
-                e[0] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
-                                   fmaxf(fmaxf(y0, y1), y2));
-                e[1] = make_float4(__int_as_float(bb.x), __int_as_float(bb.y), fminf(fminf(z0, z1), z2),
-                                   __int_as_float(f));
-                e[2] = make_float4(x0, y0, x1, y1);
-                e[3] = make_float4(x2, y2, z0, z1);
-                e[4] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
-                e[5] = make_float4(y2 - y1, x0 - x2, y0 - y2, y1 - y2);
-                e[6] = make_float4(y2 - y0, y0 - y1, x1 * y2 - x2 * y1, x2 * y0 - x0 * y2);
-                e[7] = make_float4(x0 * y1 - x1 * y0, 0.f, 0.f, 0.f);
+            for (uint32_t m = bits; m; m &= m - 1, r++) {
+                if (r < cbase) continue;
+                if (r >= cbase + CAND) break;
+                s_cand[r - cbase] = w * 32 + __builtin_ctz(m);
             }
             __syncthreads();
-            const int n = min(CAP, total - base);
-            for (int i = 0; i < n; i++) {
-                const float4 q1 = s_face[i][1];
-                const int bx = __float_as_int(q1.x), by = __float_as_int(q1.y);
-                // wave-uniform skip: face bbox misses this wave's 16x4 pixels
-                if (range_lo(bx) > wx1 || range_hi(bx) < wx0 || range_lo(by) > wy1 || range_hi(by) < wy0) continue;
-                const float4 q0 = s_face[i][0];
-                // .cu:94-97 (min/max form, exact for non-NaN faces)
-                if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) continue;
-                const float4 q2 = s_face[i][2], q3 = s_face[i][3], q4 = s_face[i][4], q5 = s_face[i][5];
-                const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
-                // .cu:107-116
-                const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
-                const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
-                if (c1 * c2 < 0) continue;
-                const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
-                if (c2 * c3 < 0) continue;
-                // .cu:124-126
-                if (depth_min < q1.z) continue;
-                const float4 q6 = s_face[i][6], q7 = s_face[i][7];
-                const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
-                // .cu:130-139
-                float w0 = yp * q4.w + xp * q5.w + q6.z;
-                float w1 = yp * q5.y + xp * q6.x + q6.w;
-                float w2 = yp * q4.y + xp * q6.y + q7.x;
-                const float ws = w0 + w1 + w2;
-                w0 /= ws;
-                w1 /= ws;
-                w2 /= ws;
-                const float zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
-                if (zp <= near || far <= zp) continue;
-                if (zp <= depth_min - delta) {  // .cu:145-148
-                    depth_min = zp;
-                    best = __float_as_int(q1.w);
-                    bf.x0 = x0; bf.y0 = y0; bf.z0 = z0;
-                    bf.x1 = x1; bf.y1 = y1; bf.z1 = z1;
-                    bf.x2 = x2; bf.y2 = y2; bf.z2 = z2;
+            const int nc = min(CAND, total - cbase);
+            for (int j0 = 0; j0 < nc; j0 += NT) {
+                const int j = j0 + t;
+                int f = 0;
+                int2 bb = make_int2(NR_EMPTY_RANGE, NR_EMPTY_RANGE);
+                if (j < nc) {
+                    f = s_cand[j];
+                    bb = bbb[f];
                 }
+                const bool keep = range_lo(bb.x) <= tx1 && range_hi(bb.x) >= tx0 && range_lo(bb.y) <= ty1 &&
+                                  range_hi(bb.y) >= ty0;
+                const unsigned long long bal = __ballot(keep);
+                const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+                if (lane == 0) s_wcnt[wid] = __popcll(bal);
+                __syncthreads();
+                int wofs = 0, tot = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int cnt = s_wcnt[i];
+                    wofs += (i < wid) ? cnt : 0;
+                    tot += cnt;
+                }
+                if (nstaged + tot > CAP) {  // block-uniform
+                    raster_staged(s_face, nstaged, xp, yp, wx0, wx1, wy0, wy1, near, far, delta, ps);
+                    nstaged = 0;
+                    __syncthreads();
+                }
+                if (keep) stage_face(s_face[nstaged + wofs + pre], frb + (long long)f * 9, f, bb);
+                nstaged += tot;
+                __syncthreads();
             }
-            __syncthreads();
         }
     }
+    if (nstaged > 0) raster_staged(s_face, nstaged, xp, yp, wx0, wx1, wy0, wy1, near, far, delta, ps);
 
     const bool inside = px < S && py < S;
-    if (inside) out.fim[((long long)b * S + py) * S + px] = best;
+    if (inside) out.fim[((long long)b * S + py) * S + px] = ps.best;
     if (!FUSED) return;
 
     float v[MAXC];
-    shade_pixel(sh, b, best, bf, xp, yp, v);
-    for (int c = 0; c < sh.C; c++) s_chan[c][ly * TW + lx] = v[c];
+    shade_pixel(sh, b, ps.best, ps.bf, xp, yp, v);
     if (!aa) {
         if (inside) {
             // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
@@ -505,6 +549,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
         }
         return;
     }
+    for (int c = 0; c < sh.C; c++) s_chan[c][ly * TW + lx] = v[c];
     __syncthreads();
     // 2x2 average of the flipped image (rasterize.py:321-328); each output pixel reads
     // internal (y0..y0+1, x0..x0+1) with y0, x0 even: a=(y0+1,x0+1) b=(y0,x0+1) c=(y0+1,x0) d=(y0,x0)
@@ -620,16 +665,31 @@ __global__ void k_diff_bwd(const float* __restrict__ img, const float* __restric
 
 // ------------------------------------------------------------------------------------------------
 // k_raster_bwd: per 32x8 tile with a 1-pixel halo.
+//   1. recompute the internal image I (all channels) and the upstream gradient G of the tile + halo
+//      into LDS (Differentiation saved images; the flip/AA backward is an index map + /4);
+//   2. per foreground pixel: the soft-gradient stencil (gx, gy) and the chain rule through the
+//      coordinate, depth and texture maps;
+//   3. the per-pixel gradients are reduced in LDS hash tables keyed by face id (9 floats, the
+//      gathered-face gradient of rasterize.py:232) and by 64-byte texel segment (4 texels x RGBA),
+//      then flushed with global float atomics whose lanes cover whole records / whole 64-byte
+//      segments (MI355X float atomics are priced per 64-byte request).
 constexpr int HW_ = TW + 2, HH_ = TH + 2, HN = HW_ * HH_;
+constexpr int FSLOTS = 256;   // face table (one pixel -> one face: at most NT distinct)
+constexpr int TSLOTS = 256;   // texel-segment table; misses fall back to direct atomics
+constexpr int PROBES = 32;
+// experiment switch for timing builds (never set in the shipped library):
+//   1 = no global flush of the LDS tables, 2 = no gradient accumulation at all
+#ifndef NR_ABLATE
+#define NR_ABLATE 0
+#endif
 
 struct BwdArgs {
     const float* __restrict__ face_records;
     const int32_t* __restrict__ fim;
-    const int32_t* __restrict__ faces_idx;
     const float* __restrict__ grad_images;
-    float* __restrict__ grad_vertices;
-    float* __restrict__ grad_tex;
-    int F, V, aa, s;
+    float* __restrict__ grad_faces;   // [B, F, 9]
+    float* __restrict__ grad_tex4;    // [Bt, HWp, 4] or null
+    int F, aa, s, HWp;
     float step;
 };
 
@@ -644,15 +704,44 @@ __device__ __forceinline__ void upstream_grad(const BwdArgs& a, int C, int b, in
     }
 }
 
+// open-addressing slot of `key` in an LDS table of (mask + 1) slots, inserting it if absent;
+// -1 when PROBES slots are taken by other keys
+__device__ __forceinline__ int lds_slot(int* keys, int mask, int key) {
+    const unsigned h = ((unsigned)key * 2654435761u) >> 7;
+    for (int i = 0; i < PROBES; i++) {
+        const int sidx = (int)((h + i) & mask);
+        const int k = __hip_atomic_load(&keys[sidx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == key) return sidx;
+        if (k == -1) {
+            const int old = atomicCAS(&keys[sidx], -1, key);
+            if (old == -1 || old == key) return sidx;
+        }
+    }
+    return -1;
+}
+
 __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) {
     __shared__ float s_I[MAXC][HN];
     __shared__ float s_G[MAXC][HN];
+    __shared__ int s_fkey[FSLOTS];
+    __shared__ __attribute__((aligned(16))) float s_fval[FSLOTS * 9];
+    __shared__ int s_tkey[TSLOTS];
+    __shared__ __attribute__((aligned(16))) float s_tval[TSLOTS * 16];
     const int b = blockIdx.y;
     const int S = g.S;
     const int C = sh.C;
+    const bool rgb = (sh.draw & NR_DRAW_RGB) != 0;
     const int tx0 = (blockIdx.x % g.tiles_x) * TW;
     const int ty0 = (blockIdx.x / g.tiles_x) * TH;
     const int t = threadIdx.x;
+
+    // clear the tables
+    s_fkey[t] = -1;
+    s_tkey[t] = -1;
+    for (int i = t; i < FSLOTS * 9 / 4; i += NT) reinterpret_cast<float4*>(s_fval)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rgb)
+        for (int i = t; i < TSLOTS * 16 / 4; i += NT) reinterpret_cast<float4*>(s_tval)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+
     int lx, ly;
     pixel_of(t, lx, ly);
     const int px = tx0 + lx, py = ty0 + ly;
@@ -698,99 +787,161 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         }
     }
     __syncthreads();
-    if (!inside || fi < 0) return;
 
-    // Differentiation.backward at this pixel
-    float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
-    for (int c = 0; c < C; c++) {
-        Im[c] = s_I[c][li - 1]; Ip[c] = s_I[c][li + 1];
-        Gm[c] = s_G[c][li - 1]; Gp[c] = s_G[c][li + 1];
-    }
-    const float gx = axis_grad(Im, I, Ip, Gm, G, Gp, px, S, C, a.step);
-    for (int c = 0; c < C; c++) {
-        Im[c] = s_I[c][li - HW_]; Ip[c] = s_I[c][li + HW_];
-        Gm[c] = s_G[c][li - HW_]; Gp[c] = s_G[c][li + HW_];
-    }
-    const float gy = axis_grad(Im, I, Ip, Gm, G, Gp, py, S, C, a.step);
+    const int bt = sh.tv.sb ? b : 0;
+    if (inside && fi >= 0) {
+        // Differentiation.backward at this pixel
+        float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
+        for (int c = 0; c < C; c++) {
+            Im[c] = s_I[c][li - 1]; Ip[c] = s_I[c][li + 1];
+            Gm[c] = s_G[c][li - 1]; Gp[c] = s_G[c][li + 1];
+        }
+        const float gx = axis_grad(Im, I, Ip, Gm, G, Gp, px, S, C, a.step);
+        for (int c = 0; c < C; c++) {
+            Im[c] = s_I[c][li - HW_]; Ip[c] = s_I[c][li + HW_];
+            Gm[c] = s_G[c][li - HW_]; Gp[c] = s_G[c][li + HW_];
+        }
+        const float gy = axis_grad(Im, I, Ip, Gm, G, Gp, py, S, C, a.step);
 
-    float w[3];
-    face_weights(xp, yp, f, w);
-    // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
-    float gF[3][3];
-    for (int k = 0; k < 3; k++) {
-        gF[k][0] = gx * w[k];
-        gF[k][1] = gy * w[k];
-        gF[k][2] = 0.f;
-    }
-    const float z[3] = {f.z0, f.z1, f.z2};
-    int c = 0;
-    if (sh.draw & NR_DRAW_RGB) {
-        TexSample s;
-        const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
-        const int bt = sh.tv.sb ? b : 0;
-        sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
-        const float gc[3] = {G[0], G[1], G[2]};
-        c = 3;
-        // bilinear: images = sum_i wt_i T_i  -> textures and weights
-        float gw[4];
-        const int HWt = sh.tv.H * sh.tv.W;
-        for (int i = 0; i < 4; i++) {
-            float acc = 0.f;
-            for (int ch = 0; ch < 3; ch++) {
-                const float tv = texel(sh.tv, bt, ch, s.idx[i]);
-                acc = (ch == 0) ? gc[ch] * tv : acc + gc[ch] * tv;
-                const float gt = gc[ch] * s.wt[i];
-                if (a.grad_tex && gt != 0.f) unsafeAtomicAdd(a.grad_tex + ((long long)bt * 3 + ch) * HWt + s.idx[i], gt);
-            }
-            gw[i] = acc;
-        }
-        const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
-        float g_x = -(gw[0] * ay);
-        g_x = g_x + gw[1] * ay;
-        g_x = g_x - gw[2] * by;
-        g_x = g_x + gw[3] * by;
-        float g_y = -(gw[0] * ax);
-        g_y = g_y - gw[1] * bx;
-        g_y = g_y + gw[2] * ax;
-        g_y = g_y + gw[3] * bx;
-        const float gp[2] = {g_x, g_y};
-        float gpr[2];
-        for (int j = 0; j < 2; j++) {
-            // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
-            const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
-            float gg = gp[j];
-            gg = (pc == hm) ? gg / 2 : (pc > hm ? 0.f : gg);
-            gg = (pr == lo) ? gg / 2 : (pr < lo ? 0.f : gg);
-            gpr[j] = gg;
-        }
-        const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
-        const float g_st = -g_dt * (s.dt * s.dt);
-        const float* fuv2 = fuv;
+        float w[3];
+        face_weights(xp, yp, f, w);
+        // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
+        float gF[9];
         for (int k = 0; k < 3; k++) {
-            float gz = 0.f;
-            for (int j = 0; j < 2; j++) {
-                const float p = w[k] * fuv2[2 * k + j];
-                gz = gz + (-(gpr[j] * s.dt)) * ((p / s.zq[k]) / s.zq[k]);
+            gF[3 * k + 0] = gx * w[k];
+            gF[3 * k + 1] = gy * w[k];
+            gF[3 * k + 2] = 0.f;
+        }
+        const float z[3] = {f.z0, f.z1, f.z2};
+        int c = 0;
+        if (rgb) {
+            TexSample s;
+            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
+            sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
+            const float gc[3] = {G[0], G[1], G[2]};
+            c = 3;
+            // bilinear: images = sum_i wt_i T_i  -> textures and weights
+            float gw[4];
+            for (int i = 0; i < 4; i++) {
+                float acc = 0.f;
+                float gt[3];
+                for (int ch = 0; ch < 3; ch++) {
+                    const float tv = texel(sh.tv, bt, ch, s.idx[i]);
+                    acc = (ch == 0) ? gc[ch] * tv : acc + gc[ch] * tv;
+                    gt[ch] = gc[ch] * s.wt[i];
+                }
+                gw[i] = acc;
+                if (NR_ABLATE & 2) {
+                    asm volatile("" ::"v"(gt[0]), "v"(gt[1]), "v"(gt[2]));
+                } else if (a.grad_tex4 && (gt[0] != 0.f || gt[1] != 0.f || gt[2] != 0.f)) {
+                    const int p = s.idx[i];
+                    const int slot = lds_slot(s_tkey, TSLOTS - 1, p >> 2);
+                    for (int ch = 0; ch < 3; ch++) {
+                        if (gt[ch] == 0.f) continue;
+                        if (slot >= 0) atomicAdd(&s_tval[slot * 16 + (p & 3) * 4 + ch], gt[ch]);
+                        else unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + p) * 4 + ch, gt[ch]);
+                    }
+                }
             }
-            gz = gz + (-g_st) * ((w[k] / s.zq[k]) / s.zq[k]);
-            gF[k][2] += gz;
+            const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
+            float g_x = -(gw[0] * ay);
+            g_x = g_x + gw[1] * ay;
+            g_x = g_x - gw[2] * by;
+            g_x = g_x + gw[3] * by;
+            float g_y = -(gw[0] * ax);
+            g_y = g_y - gw[1] * bx;
+            g_y = g_y + gw[2] * ax;
+            g_y = g_y + gw[3] * bx;
+            const float gp[2] = {g_x, g_y};
+            float gpr[2];
+            for (int j = 0; j < 2; j++) {
+                // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
+                const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
+                float gg = gp[j];
+                gg = (pc == hm) ? gg / 2 : (pc > hm ? 0.f : gg);
+                gg = (pr == lo) ? gg / 2 : (pr < lo ? 0.f : gg);
+                gpr[j] = gg;
+            }
+            const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
+            const float g_st = -g_dt * (s.dt * s.dt);
+            for (int k = 0; k < 3; k++) {
+                float gz = 0.f;
+                for (int j = 0; j < 2; j++) {
+                    const float pk = w[k] * fuv[2 * k + j];
+                    gz = gz + (-(gpr[j] * s.dt)) * ((pk / s.zq[k]) / s.zq[k]);
+                }
+                gz = gz + (-g_st) * ((w[k] / s.zq[k]) / s.zq[k]);
+                gF[3 * k + 2] += gz;
+            }
+        }
+        if (sh.draw & NR_DRAW_SILHOUETTES) c++;
+        if (sh.draw & NR_DRAW_DEPTH) {
+            const float gd = G[c];
+            const float d = I[c];
+            const float g_s = -gd * (d * d);
+            for (int k = 0; k < 3; k++) gF[3 * k + 2] += (-g_s) * ((w[k] / z[k]) / z[k]);
+        }
+        if (NR_ABLATE & 2) {
+            for (int k = 0; k < 9; k++) asm volatile("" ::"v"(gF[k]));
+        } else {
+        const int slot = lds_slot(s_fkey, FSLOTS - 1, fi);
+        for (int k = 0; k < 9; k++) {
+            if (gF[k] == 0.f) continue;
+            if (slot >= 0) atomicAdd(&s_fval[slot * 9 + k], gF[k]);
+            else unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + fi) * 9 + k, gF[k]);
+        }
         }
     }
-    if (sh.draw & NR_DRAW_SILHOUETTES) c++;
-    if (sh.draw & NR_DRAW_DEPTH) {
-        const float gd = G[c];
-        const float d = I[c];
-        const float g_s = -gd * (d * d);
-        for (int k = 0; k < 3; k++) gF[k][2] += (-g_s) * ((w[k] / z[k]) / z[k]);
+    __syncthreads();
+    if (NR_ABLATE & 3) return;
+    // flush: consecutive lanes cover one record / one 64-byte texel segment
+    for (int e = t; e < FSLOTS * 9; e += NT) {
+        const int sl = e / 9, k = e - sl * 9;
+        const int key = s_fkey[sl];
+        if (key < 0) continue;
+        const float v = s_fval[e];
+        if (v != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + k, v);
     }
-    // faces = vertices[:, faces] backward: scatter to the three corner vertices
-    float* gv = a.grad_vertices + (long long)b * a.V * 3;
-    for (int k = 0; k < 3; k++) {
-        const int vi = a.faces_idx[fi * 3 + k];
-        if (gF[k][0] != 0.f) unsafeAtomicAdd(gv + vi * 3 + 0, gF[k][0]);
-        if (gF[k][1] != 0.f) unsafeAtomicAdd(gv + vi * 3 + 1, gF[k][1]);
-        if (gF[k][2] != 0.f) unsafeAtomicAdd(gv + vi * 3 + 2, gF[k][2]);
+    if (rgb && a.grad_tex4) {
+        for (int e = t; e < TSLOTS * 16; e += NT) {
+            const int key = s_tkey[e >> 4];
+            if (key < 0) continue;
+            const float v = s_tval[e];
+            if (v != 0.f) unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)key * 4) * 4 + (e & 15), v);
+        }
     }
+}
+
+// gathered-face gradient -> vertex gradient: gV[b, v] = sum over (f, k) with faces[f, k] = v of gF[b, f, k]
+// (the index backward of rasterize.py:232), through a CSR adjacency built once per faces tensor.
+__global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __restrict__ off,
+                              const int32_t* __restrict__ ent, float* __restrict__ gV, int F, int V, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / V), v = (int)(i % V);
+    const float* base = gF + (long long)b * F * 9;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int e = off[v]; e < off[v + 1]; e++) {
+        const float* r = base + (long long)ent[e] * 3;  // entry = 3 f + k
+        s0 += r[0];
+        s1 += r[1];
+        s2 += r[2];
+    }
+    gV[i * 3 + 0] = s0;
+    gV[i * 3 + 1] = s1;
+    gV[i * 3 + 2] = s2;
+}
+
+// [Bt, HWp, 4] accumulation layout -> [Bt, 3, H, W]
+__global__ void k_tex_out(const float* __restrict__ g4, float* __restrict__ out, int HW, int HWp, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const long long bt = i / HW;
+    const int p = (int)(i % HW);
+    const float4 v = reinterpret_cast<const float4*>(g4)[bt * HWp + p];
+    out[(bt * 3 + 0) * HW + p] = v.x;
+    out[(bt * 3 + 1) * HW + p] = v.y;
+    out[(bt * 3 + 2) * HW + p] = v.z;
 }
 
 int validate_raster(const NrRasterArgs* a, bool need_workspace) {
@@ -810,8 +961,8 @@ int validate_raster(const NrRasterArgs* a, bool need_workspace) {
         if (a->tex_height <= 0 || a->tex_width <= 0) return fail(NR_ERR_ARGS, "bad texture size");
     }
     const Geom g = make_geom(a->num_faces, S);
-    if (need_workspace && (!a->workspace || a->workspace_bytes < ws_bbox_bytes(a->batch_size, a->num_faces) +
-                                                                  ws_mask_bytes(a->batch_size, g)))
+    const size_t need = ws_bbox_bytes(a->batch_size, a->num_faces) + ws_mask_bytes(a->batch_size, g);
+    if (need_workspace && need > 0 && (!a->workspace || a->workspace_bytes < need))
         return fail(NR_ERR_WORKSPACE, "workspace missing or too small");
     return NR_OK;
 }
@@ -948,30 +1099,62 @@ int nr_rasterize_forward(const NrRasterArgs* a, float* images, void* stream) {
                           a->workspace_bytes, (hipStream_t)stream, a, images);
 }
 
+size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int texture_items, int tex_height,
+                                   int tex_width) {
+    const size_t hwp = ((size_t)tex_height * tex_width + 3) & ~size_t(3);
+    return align_up((size_t)batch_size * num_faces * 9 * 4) + align_up((size_t)texture_items * hwp * 16);
+}
+
 int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float* grad_vertices, float* grad_textures,
-                          void* stream) {
+                          void* workspace, size_t workspace_bytes, void* stream) {
     int e = validate_raster(a, false);
     if (e) return e;
     if (a->batch_size == 0) return NR_OK;
     if (!grad_images || !grad_vertices) return fail(NR_ERR_ARGS, "null gradient buffers");
+    if (a->num_faces > 0 && (!a->vertex_offsets || !a->vertex_faces))
+        return fail(NR_ERR_ARGS, "missing vertex adjacency (vertex_offsets / vertex_faces)");
+    const bool rgb = (a->draw_flags & NR_DRAW_RGB) && grad_textures;
+    const int tex_items = rgb ? (a->tex_stride_b ? a->batch_size : 1) : 0;
+    const size_t need = nr_backward_workspace_bytes(a->batch_size, a->num_faces, tex_items, a->tex_height, a->tex_width);
+    if (need > 0 && (!workspace || workspace_bytes < need))
+        return fail(NR_ERR_WORKSPACE, "backward workspace missing or too small");
+    hipStream_t st = (hipStream_t)stream;
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
     const Geom g = make_geom(a->num_faces, S);
+    float* gF = (float*)workspace;
+    const size_t gF_bytes = align_up((size_t)a->batch_size * a->num_faces * 9 * 4);
+    float* g4 = (float*)((char*)workspace + gF_bytes);
+    const int HW = a->tex_height * a->tex_width;
+    const int HWp = (HW + 3) & ~3;
+    if (need > 0 && hipMemsetAsync(workspace, 0, need, st) != hipSuccess) return check_launch("hipMemsetAsync");
     BwdArgs ba;
     ba.face_records = a->face_records;
     ba.fim = a->face_index;
-    ba.faces_idx = a->faces;
     ba.grad_images = grad_images;
-    ba.grad_vertices = grad_vertices;
-    ba.grad_tex = (a->draw_flags & NR_DRAW_RGB) ? grad_textures : nullptr;
+    ba.grad_faces = gF;
+    ba.grad_tex4 = rgb ? g4 : nullptr;
     ba.F = a->num_faces;
-    ba.V = a->num_vertices;
     ba.aa = a->anti_aliasing;
     ba.s = a->image_size;
+    ba.HWp = HWp;
     ba.step = (float)(2. / S);
     Shade sh = make_shade(a);
-    hipLaunchKernelGGL(k_raster_bwd, dim3(g.tiles_x * g.tiles_y, a->batch_size), dim3(NT), 0, (hipStream_t)stream, ba,
-                       g, sh);
-    return check_launch("k_raster_bwd");
+    hipLaunchKernelGGL(k_raster_bwd, dim3(g.tiles_x * g.tiles_y, a->batch_size), dim3(NT), 0, st, ba, g, sh);
+    e = check_launch("k_raster_bwd");
+    if (e) return e;
+    const long long nv = (long long)a->batch_size * a->num_vertices;
+    if (nv > 0) {
+        hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gF, a->vertex_offsets,
+                           a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv);
+        e = check_launch("k_vertex_grad");
+        if (e) return e;
+    }
+    if (rgb) {
+        const long long nt = (long long)tex_items * HW;
+        hipLaunchKernelGGL(k_tex_out, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, g4, grad_textures, HW, HWp, nt);
+        e = check_launch("k_tex_out");
+    }
+    return e;
 }
 
 }  // extern "C"

@@ -140,12 +140,34 @@ def _faces_i32(faces, device, bound, what):
     return f
 
 
+_adjacency = {}
+
+
+def _vertex_adjacency(faces_i32, V):
+    """CSR vertex -> face corners (3 f + k) for the backward's vertex gather, built on the host
+    with a stable sort (deterministic summation order) and cached per (storage, version)."""
+    key = (faces_i32.data_ptr(), faces_i32._version, faces_i32.shape[0], V, faces_i32.device)
+    hit = _adjacency.get("faces")
+    if hit is not None and hit[0] == key:
+        return hit[1], hit[2]
+    import numpy as np
+    flat = faces_i32.reshape(-1).cpu().numpy().astype(np.int64)
+    order = np.argsort(flat, kind="stable").astype(np.int32)
+    counts = np.bincount(flat, minlength=V)
+    offsets = np.zeros(V + 1, np.int32)
+    np.cumsum(counts, out=offsets[1:])
+    off = torch.as_tensor(offsets, device=faces_i32.device)
+    ent = torch.as_tensor(order, device=faces_i32.device)
+    _adjacency["faces"] = (key, off, ent, faces_i32)  # keep faces_i32 alive: its storage is the key
+    return off, ent
+
+
 class _Cfg:
     __slots__ = ("image_size", "aa", "backside", "flags", "near", "far", "eps", "C", "V", "F", "tex_shared",
-                 "tex_hw", "vt_shared", "Vt", "B")
+                 "tex_hw", "vt_shared", "Vt", "B", "tex_view")
 
 
-def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws):
+def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj=None):
     a = _lib.NrRasterArgs()
     a.batch_size = cfg.B
     a.num_vertices = cfg.V
@@ -165,18 +187,20 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws):
     if ws is not None:
         a.workspace = ws.data_ptr()
         a.workspace_bytes = ws.numel()
-    else:  # the backward does not use the workspace
+    else:  # the backward does not use the forward workspace
         a.workspace = None
         a.workspace_bytes = 0
+    if adj is not None:
+        a.vertex_offsets = adj[0].data_ptr()
+        a.vertex_faces = adj[1].data_ptr()
     if cfg.flags & _lib.NR_DRAW_RGB:
         a.vertices_textures = vt.data_ptr()
         a.vt_batch_stride = vt.stride(0)
         a.num_vertices_textures = cfg.Vt
         a.faces_textures = ft.data_ptr()
-        a.textures = tex.data_ptr()
-        a.tex_stride_b = tex.stride(0)
-        a.tex_stride_c = tex.stride(1)
-        a.tex_stride_p = tex.stride(3)
+        tv = cfg.tex_view  # (data_ptr offset in elements, strides) of the [B, 3, H, W] view read
+        a.textures = tex.data_ptr() + 4 * tv[0]
+        a.tex_stride_b, a.tex_stride_c, a.tex_stride_p = tv[1], tv[2], tv[3]
         a.tex_height, a.tex_width = cfg.tex_hw
         a.face_uv = face_uv.data_ptr()
     return a
@@ -215,20 +239,27 @@ class Rasterize(torch.autograd.Function):
         cfg = ctx.cfg
         vertices, textures, vt, faces, ft, face_records, face_uv, fim = ctx.saved_tensors
         grad_images = grad_images.contiguous()
-        gv = torch.zeros_like(vertices)
+        L = _lib.lib()
+        dev = vertices.device
+        gv = torch.empty_like(vertices)
         gt = None
         want_tex = bool(cfg.flags & _lib.NR_DRAW_RGB) and ctx.needs_input_grad[1]
+        tex_items = 0
         if want_tex:
             H, W = cfg.tex_hw
-            gt = torch.zeros((1 if cfg.tex_shared else cfg.B, 3, H, W), dtype=torch.float32, device=vertices.device)
-        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None)
-        with torch.cuda.device(vertices.device):
-            _lib.check(_lib.lib().nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt),
-                                                         _lib.stream_of(vertices)), "nr_rasterize_backward")
-        if gt is not None and cfg.tex_shared and cfg.B > 1:
-            # textures is a batch-expanded view: its gradient is summed over the batch by the
-            # expand's backward; hand back the batch total spread evenly
-            gt = (gt / cfg.B).expand(textures.shape)
+            tex_items = 1 if cfg.tex_shared else cfg.B
+            gt = torch.empty((tex_items, 3, H, W), dtype=torch.float32, device=dev)
+        H, W = cfg.tex_hw
+        ws = torch.empty(L.nr_backward_workspace_bytes(cfg.B, cfg.F, tex_items, H, W), dtype=torch.uint8, device=dev)
+        adj = _vertex_adjacency(faces, cfg.V)
+        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj)
+        with torch.cuda.device(dev):
+            _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),
+                                               ws.numel(), _lib.stream_of(vertices)), "nr_rasterize_backward")
+        if gt is not None:
+            # the Function's texture input is [B, 3, H, W], or the single [3, H, W] / [1, 3, H, W]
+            # source of a shared texture (see rasterize_core): same element count as gt either way
+            gt = gt.reshape(textures.shape)
         return (gv if ctx.needs_input_grad[0] else None), gt, None, None, None, None
 
 
@@ -282,6 +313,7 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
     tex = vt = ft = None
     cfg.tex_shared = cfg.vt_shared = False
     cfg.tex_hw = (0, 0)
+    cfg.tex_view = (0, 0, 0, 0)
     cfg.Vt = 0
     if hyperparams.draw_rgb:
         vt = params.vertices_textures
@@ -304,13 +336,27 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
         tex = tex.float()
         if tex.shape[0] not in (1, cfg.B):
             raise AssertionError("textures batch must be 1 or %d" % cfg.B)
-        if tex.shape[0] == 1 and cfg.B > 1:
-            tex = tex.expand(cfg.B, *tex.shape[1:])
         H, W = tex.shape[2], tex.shape[3]
-        if tex.stride(2) != W * tex.stride(3):
+        if tex.shape[0] > 1 and tex.stride(0) != 0 and tex.stride(2) != W * tex.stride(3):
             tex = tex.contiguous()
         cfg.tex_hw = (H, W)
-        cfg.tex_shared = tex.stride(0) == 0 or cfg.B == 1
+        cfg.tex_shared = tex.shape[0] == 1 or tex.stride(0) == 0
+        if cfg.tex_shared:
+            # one texture for every item.  A batch-expanded view (tex[None].expand(B, ...), the
+            # reference tests' idiom) is handed to the Function as its [3, H, W] source so that the
+            # texture gradient is returned once, not B times through expand's backward.
+            item = tex[0]
+            base = tex._base if tex._is_view() else None
+            if (base is not None and base.numel() == 3 * H * W and base.is_contiguous()
+                    and item.is_contiguous() and item.data_ptr() == base.data_ptr()):
+                tex = base
+            elif not item.is_contiguous():
+                tex = item.contiguous()[None]
+            elif tex.shape[0] != 1:
+                tex = item[None]
+            cfg.tex_view = (0, 0, H * W, 1)
+        else:
+            cfg.tex_view = (0, tex.stride(0), tex.stride(1), tex.stride(3))
     else:
         tex = torch.empty(0, device=dev)
     if vt is None:

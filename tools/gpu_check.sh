@@ -1,13 +1,18 @@
+# usage: bash tools/gpu_check.sh <tag>: GPU tests, smoke, short bench, rocprofv3 kernel stats
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-nproc > gpurun_out/nproc.txt; lscpu | grep "Model name" >> gpurun_out/nproc.txt
-timeout -k 10 900 python -m pytest tests -m gpu -q -x --timeout 600 -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
-rc=$?
-echo "pytest rc=$rc"
+export TMPDIR=/tmp
+TAG=${1:-check}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider > $OUT/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-rc=$?; echo "smoke rc=$rc"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -1 $OUT/smoke.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 5 > gpurun_out/bench1.log 2>&1
-echo "bench rc=$?"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 5 > $OUT/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 $OUT/bench.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1
+echo "rocprof rc=$?"

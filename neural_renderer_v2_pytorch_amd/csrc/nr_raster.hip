@@ -12,8 +12,8 @@
 //   k_face_setup     one block per (128 faces, item): gather the faces from vertices (rasterize.py:232),
 //                    per-face screen bbox + face-level rejects, texture-uv gather, and the coarse-bin
 //                    face bitmasks (64x64-pixel bins, bit f set when face f may touch the bin).
-//   k_raster_fwd     one block per 32x8-pixel tile: compacts the coarse bin's faces that touch the
-//                    tile, in face order, into LDS (ballot-free block scan), scans them per pixel,
+//   k_raster_fwd     one block per 32x32-pixel coarse bin: stages the bin's candidate faces in face
+//                    order into LDS, each wave walks (ballot) the faces touching its pixels in order,
 //                    then shades rgb/sil/depth and writes fim + the flipped, 2x2-averaged output.
 //   backward         k_raster_bwd: one block per tile with a 1-pixel halo: recomputes the internal
 //                    image from fim, applies Differentiation.backward's stencil, and chains the
@@ -36,7 +36,7 @@ namespace {
 constexpr int TW = 32;             // tile width  (internal pixels)
 constexpr int TH = 8;              // tile height
 constexpr int NT = TW * TH;        // threads per raster block, one pixel each
-constexpr int COARSE = 64;         // coarse bin edge (pixels); multiple of TW and TH
+constexpr int COARSE = 32;         // coarse bin edge (pixels) = forward block region; = TW, multiple of TH
 constexpr int CAP = 256;           // faces staged in LDS per round
 constexpr int SETUP_FACES = 128;   // faces per setup block (4 bitmask words)
 constexpr int MAXC = 5;            // max output channels
@@ -228,27 +228,31 @@ struct Shade {
     long long uv_bstride;  // F*6 or 0
 };
 
-// All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth).
+// All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth), written
+// to compile-time slots of out[MAXC] (runtime-indexed register arrays would spill to scratch).
 __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, float xp, float yp,
                                             float* out) {
-    int c = 0;
-    if (fi < 0) {
-        for (int k = 0; k < sh.C; k++) out[k] = 0.f;
-        return;
+    const bool R = (sh.draw & NR_DRAW_RGB) != 0, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
+    float r = 0.f, gg = 0.f, bb = 0.f, sil = 0.f, dep = 0.f;
+    if (fi >= 0) {
+        float w[3];
+        face_weights(xp, yp, f, w);
+        if (R) {
+            TexSample s;
+            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
+            sample_texture(f, w, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s);
+            r = s.rgb[0];
+            gg = s.rgb[1];
+            bb = s.rgb[2];
+        }
+        sil = 1.f;
+        if (sh.draw & NR_DRAW_DEPTH) dep = depth_value(f, w);
     }
-    float w[3];
-    face_weights(xp, yp, f, w);
-    if (sh.draw & NR_DRAW_RGB) {
-        TexSample s;
-        const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
-        const int bt = sh.tv.sb ? b : 0;
-        sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
-        out[c++] = s.rgb[0];
-        out[c++] = s.rgb[1];
-        out[c++] = s.rgb[2];
-    }
-    if (sh.draw & NR_DRAW_SILHOUETTES) out[c++] = 1.f;
-    if (sh.draw & NR_DRAW_DEPTH) out[c++] = depth_value(f, w);
+    out[0] = R ? r : (Sl ? sil : dep);
+    out[1] = R ? gg : dep;
+    out[2] = bb;
+    out[3] = Sl ? sil : dep;
+    out[4] = dep;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -362,18 +366,29 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_raster_fwd: per 32x8 tile.
-//   face list: the coarse bin's bitmask words are expanded (block scan over popcounts) into an
-//   ordered candidate list in LDS; candidates are then tested against the tile 256 at a time (one
-//   bbox load per thread) and the survivors appended in order (ballot + popcount prefix) to the
-//   LDS face stage, which is rasterised whenever it would overflow -- so every pixel sees its
-//   faces in ascending index order, as the reference's sequential loop does.
+// k_raster_fwd: one block per 32x32-pixel coarse bin (the bitmask granularity), 4 pixels per thread
+// (4 sub-tiles of 32x8; in each, the 4 waves own 16x4 pixel blocks).
+//   1. the bin's bitmask words are expanded (block scan over popcounts) into the ordered list of
+//      candidate faces;
+//   2. up to FCAP candidates at a time are staged into LDS in ascending face order (one face per
+//      thread, one global load stage);
+//   3. per sub-tile, each wave ballots which staged faces touch its 16x4 pixels and walks the set
+//      bits in order (scalar loop), running the reference's per-face test for its pixel -- every
+//      pixel therefore sees its candidate faces in ascending index order, as the reference's
+//      sequential loop does (.cu:82-149), and the per-pixel state stays in registers across rounds;
+//   4. shading of the 4 pixels (weights, texture, depth) and the flipped, 2x2-averaged output
+//      written through LDS in 64-byte rows.
 //   LDS face record (7 x float4):
 //     0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
 //     4: z2 A=x1-x0 B=y1-y0 C=x2-x1 | 5: D=y2-y1 E=x0-x2 F=y0-y2 k0 | 6: k1 k2 - -
 //   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
-constexpr int CAND = 1024;
-constexpr int FREC = 7;
+constexpr int CAND = 512;                       // candidate ids expanded per round
+constexpr int FCAP = 128;                       // faces staged per round
+constexpr int FREC = 7;                         // float4 per staged face
+constexpr int NSUB = (COARSE * COARSE) / NT;    // pixels per thread (4)
+constexpr int FWD_LDS_FACES = FCAP * FREC * 16 + CAND * 4;
+constexpr int FWD_LDS_CHAN = MAXC * COARSE * COARSE * 4;
+constexpr int FWD_LDS = FWD_LDS_FACES > FWD_LDS_CHAN ? FWD_LDS_FACES : FWD_LDS_CHAN;
 
 struct FwdOut {
     float* images;   // [B, C, s, s] (FUSED only)
@@ -381,58 +396,44 @@ struct FwdOut {
 };
 
 __device__ __forceinline__ void pixel_of(int t, int& lx, int& ly) {
-    // 4 waves as a 2x2 grid of 16x4 pixel blocks
+    // 4 waves as a 2x2 grid of 16x4 pixel blocks of a 32x8 tile
     const int w = t >> 6, l = t & 63;
     lx = (w & 1) * 16 + (l & 15);
     ly = (w >> 1) * 4 + (l >> 4);
 }
 
-struct PixState {
-    float depth_min;
-    int best;
-    Face bf;
-};
-
-// the reference's per-face test sequence (.cu:94-148) over n staged faces
-__device__ __forceinline__ void raster_staged(const float4 (*s_face)[FREC], int n, float xp, float yp, int wx0, int wx1,
-                                              int wy0, int wy1, float near, float far, float delta, PixState& ps) {
-    for (int i = 0; i < n; i++) {
-        const float4 q1 = s_face[i][1];
-        const int bx = __float_as_int(q1.x), by = __float_as_int(q1.y);
-        // wave-uniform skip: face bbox misses this wave's 16x4 pixels
-        if (range_lo(bx) > wx1 || range_hi(bx) < wx0 || range_lo(by) > wy1 || range_hi(by) < wy0) continue;
-        const float4 q0 = s_face[i][0];
-        // .cu:94-97 (min/max form, exact for non-NaN faces)
-        if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) continue;
-        const float4 q2 = s_face[i][2], q3 = s_face[i][3], q4 = s_face[i][4], q5 = s_face[i][5];
-        const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
-        // .cu:107-116
-        const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
-        const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
-        if (c1 * c2 < 0) continue;
-        const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
-        if (c2 * c3 < 0) continue;
-        // .cu:124-126
-        if (ps.depth_min < q1.z) continue;
-        const float4 q6 = s_face[i][6];
-        const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
-        // .cu:130-139
-        float w0 = (yp * q4.w - xp * q5.x) + q5.w;
-        float w1 = (yp * q5.y - xp * q5.z) + q6.x;
-        float w2 = (yp * q4.y - xp * q4.z) + q6.y;
-        const float ws = w0 + w1 + w2;
-        w0 /= ws;
-        w1 /= ws;
-        w2 /= ws;
-        const float zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
-        if (zp <= near || far <= zp) continue;
-        if (zp <= ps.depth_min - delta) {  // .cu:145-148
-            ps.depth_min = zp;
-            ps.best = __float_as_int(q1.w);
-            ps.bf.x0 = x0; ps.bf.y0 = y0; ps.bf.z0 = z0;
-            ps.bf.x1 = x1; ps.bf.y1 = y1; ps.bf.z1 = z1;
-            ps.bf.x2 = x2; ps.bf.y2 = y2; ps.bf.z2 = z2;
-        }
+// the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel
+__device__ __forceinline__ void face_test(const float4* e, float xp, float yp, float near, float far, float delta,
+                                          float& depth_min, int& best) {
+    const float4 q0 = e[0];
+    // .cu:94-97 (min/max form, exact for non-NaN faces)
+    if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
+    const float4 q2 = e[2], q3 = e[3], q4 = e[4], q5 = e[5];
+    const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
+    // .cu:107-116
+    const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
+    const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
+    if (c1 * c2 < 0) return;
+    const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
+    if (c2 * c3 < 0) return;
+    const float4 q1 = e[1];
+    // .cu:124-126
+    if (depth_min < q1.z) return;
+    const float4 q6 = e[6];
+    const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
+    // .cu:130-139
+    float w0 = (yp * q4.w - xp * q5.x) + q5.w;
+    float w1 = (yp * q5.y - xp * q5.z) + q6.x;
+    float w2 = (yp * q4.y - xp * q4.z) + q6.y;
+    const float ws = w0 + w1 + w2;
+    w0 /= ws;
+    w1 /= ws;
+    w2 /= ws;
+    const float zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
+    if (zp <= near || far <= zp) return;
+    if (zp <= depth_min - delta) {  // .cu:145-148
+        depth_min = zp;
+        best = __float_as_int(q1.w);
     }
 }
 
@@ -453,38 +454,38 @@ template <bool FUSED>
 __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, const int2* __restrict__ bbox,
                                                   const uint32_t* __restrict__ mask, int F, Geom g, float near,
                                                   float far, float delta, Shade sh, int aa, FwdOut out) {
-    __shared__ float4 s_face[CAP][FREC];
-    __shared__ int s_cand[CAND];
+    __shared__ __attribute__((aligned(16))) unsigned char s_raw[FWD_LDS];
     __shared__ int s_scan[4];
-    __shared__ int s_wcnt[4];
-    __shared__ float s_chan[FUSED ? MAXC : 1][NT];
+    float4(*s_face)[FREC] = reinterpret_cast<float4(*)[FREC]>(s_raw);
+    int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
+    float* s_chan = reinterpret_cast<float*>(s_raw);  // after rasterisation: [C][NSUB][NT]
 
     const int b = blockIdx.y;
     const int S = g.S;
-    const int tx0 = (blockIdx.x % g.tiles_x) * TW;
-    const int ty0 = (blockIdx.x / g.tiles_x) * TH;
+    const int bx0 = (blockIdx.x % g.nbx) * COARSE;
+    const int by0 = (blockIdx.x / g.nbx) * COARSE;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     int lx, ly;
     pixel_of(t, lx, ly);
-    const int px = tx0 + lx, py = ty0 + ly;
+    const int px = bx0 + lx;
     const float xp = pix_center(px, S);
-    const float yp = pix_center(py, S);
-    // this wave's pixel rectangle, for the wave-uniform face skip
-    const int wx0 = tx0 + (wid & 1) * 16, wy0 = ty0 + (wid >> 1) * 4;
-    const int wx1 = wx0 + 15, wy1 = wy0 + 3;
-    const int tx1 = tx0 + TW - 1, ty1 = ty0 + TH - 1;
+    float yp[NSUB];
+    float depth_min[NSUB];
+    int best[NSUB];
+#pragma unroll
+    for (int k = 0; k < NSUB; k++) {
+        yp[k] = pix_center(by0 + TH * k + ly, S);
+        depth_min[k] = far;
+        best[k] = -1;
+    }
+    // this wave's 16x4 pixel block in sub-tile 0 (sub-tile k adds TH * k to y)
+    const int wx0 = bx0 + (wid & 1) * 16, wx1 = wx0 + 15;
+    const int wy0 = by0 + (wid >> 1) * 4;
 
-    PixState ps;
-    ps.depth_min = far;
-    ps.best = -1;
-    ps.bf = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-
-    const int bin = (ty0 / COARSE) * g.nbx + (tx0 / COARSE);
-    const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
+    const uint32_t* words = mask + ((long long)b * g.nbins + blockIdx.x) * g.nwords;
     const int2* bbb = bbox + (long long)b * F;
     const float* frb = face_records + (long long)b * F * 9;
-    int nstaged = 0;
 
     for (int wbase = 0; wbase < g.nwords; wbase += NT) {
         const int w = wbase + t;
@@ -501,68 +502,84 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
             }
             __syncthreads();
             const int nc = min(CAND, total - cbase);
-            for (int j0 = 0; j0 < nc; j0 += NT) {
-                const int j = j0 + t;
-                int f = 0;
-                int2 bb = make_int2(NR_EMPTY_RANGE, NR_EMPTY_RANGE);
-                if (j < nc) {
-                    f = s_cand[j];
-                    bb = bbb[f];
+            for (int j0 = 0; j0 < nc; j0 += FCAP) {
+                const int n = min(FCAP, nc - j0);
+                if (t < n) {
+                    const int f = s_cand[j0 + t];
+                    stage_face(s_face[t], frb + (long long)f * 9, f, bbb[f]);
                 }
-                const bool keep = range_lo(bb.x) <= tx1 && range_hi(bb.x) >= tx0 && range_lo(bb.y) <= ty1 &&
-                                  range_hi(bb.y) >= ty0;
-                const unsigned long long bal = __ballot(keep);
-                const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-                if (lane == 0) s_wcnt[wid] = __popcll(bal);
                 __syncthreads();
-                int wofs = 0, tot = 0;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int cnt = s_wcnt[i];
-                    wofs += (i < wid) ? cnt : 0;
-                    tot += cnt;
+                for (int k = 0; k < NSUB; k++) {
+                    const int y0w = wy0 + TH * k, y1w = y0w + 3;
+                    for (int c0 = 0; c0 < n; c0 += 64) {
+                        bool hit = false;
+                        if (c0 + lane < n) {
+                            const float4 q1 = s_face[c0 + lane][1];
+                            const int fbx = __float_as_int(q1.x), fby = __float_as_int(q1.y);
+                            hit = range_lo(fbx) <= wx1 && range_hi(fbx) >= wx0 && range_lo(fby) <= y1w &&
+                                  range_hi(fby) >= y0w;
+                        }
+                        // faces touching this wave's pixels, walked in ascending order
+                        for (unsigned long long m = __ballot(hit); m; m &= m - 1)
+                            face_test(s_face[c0 + __builtin_ctzll(m)], xp, yp[k], near, far, delta, depth_min[k],
+                                      best[k]);
+                    }
                 }
-                if (nstaged + tot > CAP) {  // block-uniform
-                    raster_staged(s_face, nstaged, xp, yp, wx0, wx1, wy0, wy1, near, far, delta, ps);
-                    nstaged = 0;
-                    __syncthreads();
-                }
-                if (keep) stage_face(s_face[nstaged + wofs + pre], frb + (long long)f * 9, f, bb);
-                nstaged += tot;
                 __syncthreads();
             }
         }
     }
-    if (nstaged > 0) raster_staged(s_face, nstaged, xp, yp, wx0, wx1, wy0, wy1, near, far, delta, ps);
 
-    const bool inside = px < S && py < S;
-    if (inside) out.fim[((long long)b * S + py) * S + px] = ps.best;
+#pragma unroll
+    for (int k = 0; k < NSUB; k++) {
+        const int py = by0 + TH * k + ly;
+        if (px < S && py < S) out.fim[((long long)b * S + py) * S + px] = best[k];
+    }
     if (!FUSED) return;
 
-    float v[MAXC];
-    shade_pixel(sh, b, ps.best, ps.bf, xp, yp, v);
+    // shading: all four pixels' loads are independent
+    float v[NSUB][MAXC];
+#pragma unroll
+    for (int k = 0; k < NSUB; k++) {
+        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (best[k] >= 0) f = load_face(frb + (long long)best[k] * 9);
+        shade_pixel(sh, b, best[k], f, xp, yp[k], v[k]);
+    }
     if (!aa) {
-        if (inside) {
-            // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
-            for (int c = 0; c < sh.C; c++)
-                out.images[(((long long)b * sh.C + c) * S + (S - 1 - py)) * S + (S - 1 - px)] = v[c];
+#pragma unroll
+        for (int k = 0; k < NSUB; k++) {
+            const int py = by0 + TH * k + ly;
+            if (px < S && py < S) {
+                // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
+#pragma unroll
+                for (int c = 0; c < MAXC; c++)
+                    if (c < sh.C)
+                        out.images[(((long long)b * sh.C + c) * S + (S - 1 - py)) * S + (S - 1 - px)] = v[k][c];
+            }
         }
         return;
     }
-    for (int c = 0; c < sh.C; c++) s_chan[c][ly * TW + lx] = v[c];
+    __syncthreads();  // s_chan aliases the face stage
+#pragma unroll
+    for (int k = 0; k < NSUB; k++)
+#pragma unroll
+        for (int c = 0; c < MAXC; c++)
+            if (c < sh.C) s_chan[(c * NSUB + k) * NT + ly * TW + lx] = v[k][c];
     __syncthreads();
-    // 2x2 average of the flipped image (rasterize.py:321-328); each output pixel reads
-    // internal (y0..y0+1, x0..x0+1) with y0, x0 even: a=(y0+1,x0+1) b=(y0,x0+1) c=(y0+1,x0) d=(y0,x0)
-    if (t < (TW / 2) * (TH / 2)) {
-        const int ox = t % (TW / 2), oy = t / (TW / 2);
-        const int ix = tx0 + 2 * ox, iy = ty0 + 2 * oy;
+    // 2x2 average of the flipped image (rasterize.py:321-328): output pixel (ox, oy) of the bin reads
+    // internal rows iy, iy+1 and columns ix, ix+1 (iy, ix even): a=(iy+1,ix+1) b=(iy,ix+1) c=(iy+1,ix) d=(iy,ix)
+    {
+        const int ox = t % (COARSE / 2), oy = t / (COARSE / 2);
+        const int ix = bx0 + 2 * ox, iy = by0 + 2 * oy;
         if (ix < S && iy < S) {
             const int s = S / 2;
             const int oi = (S - 2 - iy) / 2, oj = (S - 2 - ix) / 2;
-            const int l00 = (2 * oy) * TW + 2 * ox;
+            const int k = (2 * oy) / TH;
+            const int l00 = ((2 * oy) % TH) * TW + 2 * ox;
             for (int c = 0; c < sh.C; c++) {
-                const float a = s_chan[c][l00 + TW + 1], bq = s_chan[c][l00 + 1];
-                const float cq = s_chan[c][l00 + TW], d = s_chan[c][l00];
+                const float* sc = s_chan + (c * NSUB + k) * NT;
+                const float a = sc[l00 + TW + 1], bq = sc[l00 + 1], cq = sc[l00 + TW], d = sc[l00];
                 out.images[(((long long)b * sh.C + c) * s + oi) * s + oj] = (((a + bq) + cq) + d) / 4.f;
             }
         }
@@ -602,8 +619,18 @@ __global__ void k_mask_fg(const int32_t* __restrict__ fi, const float* __restric
 //   R[i] = r[i] + r[i-1], L[i] = l[i-1] + l[i] (missing terms 0), then maximum(R, L)
 __device__ __forceinline__ float pair_dot(const float* a, const float* b, const float* g, int C) {
     float s = (a[0] - b[0]) * g[0];
-    for (int c = 1; c < C; c++) s = s + (a[c] - b[c]) * g[c];
+#pragma unroll
+    for (int c = 1; c < MAXC; c++)
+        if (c < C) s = s + (a[c] - b[c]) * g[c];
     return s;
+}
+
+// arr[i] for a runtime i < MAXC without a runtime-indexed (scratch) access
+__device__ __forceinline__ float pick(const float* arr, int i) {
+    float v = arr[0];
+#pragma unroll
+    for (int c = 1; c < MAXC; c++) v = (i == c) ? arr[c] : v;
+    return v;
 }
 
 __device__ __forceinline__ float pick_grad(float R, float L) {
@@ -697,10 +724,13 @@ __device__ __forceinline__ void upstream_grad(const BwdArgs& a, int C, int b, in
     if (a.aa) {
         const int s = a.s;
         const int oi = (S - 1 - y) >> 1, oj = (S - 1 - x) >> 1;
-        for (int c = 0; c < C; c++) G[c] = a.grad_images[(((long long)b * C + c) * s + oi) * s + oj] / 4.f;
+#pragma unroll
+        for (int c = 0; c < MAXC; c++)
+            G[c] = c < C ? a.grad_images[(((long long)b * C + c) * s + oi) * s + oj] / 4.f : 0.f;
     } else {
-        for (int c = 0; c < C; c++)
-            G[c] = a.grad_images[(((long long)b * C + c) * S + (S - 1 - y)) * S + (S - 1 - x)];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++)
+            G[c] = c < C ? a.grad_images[(((long long)b * C + c) * S + (S - 1 - y)) * S + (S - 1 - x)] : 0.f;
     }
 }
 
@@ -751,6 +781,7 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
     int fi = -1;
     Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     float I[MAXC], G[MAXC];
+    #pragma unroll
     for (int c = 0; c < MAXC; c++) I[c] = G[c] = 0.f;
     if (inside) {
         fi = a.fim[((long long)b * S + py) * S + px];
@@ -759,9 +790,12 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         upstream_grad(a, C, b, py, px, S, G);
     }
     const int li = (ly + 1) * HW_ + (lx + 1);
-    for (int c = 0; c < C; c++) {
-        s_I[c][li] = I[c];
-        s_G[c][li] = G[c];
+#pragma unroll
+    for (int c = 0; c < MAXC; c++) {
+        if (c < C) {
+            s_I[c][li] = I[c];
+            s_G[c][li] = G[c];
+        }
     }
     // halo ring: 2 rows of HW_ + 2 columns of TH
     if (t < 2 * HW_ + 2 * TH) {
@@ -772,6 +806,7 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         else { hy = 1 + (t - 2 * HW_ - TH); hx = HW_ - 1; }
         const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
         float hI[MAXC], hG[MAXC];
+        #pragma unroll
         for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
         if (y >= 0 && y < S && x >= 0 && x < S) {
             const int hf = a.fim[((long long)b * S + y) * S + x];
@@ -781,9 +816,12 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
             upstream_grad(a, C, b, y, x, S, hG);
         }
         const int hl = hy * HW_ + hx;
-        for (int c = 0; c < C; c++) {
-            s_I[c][hl] = hI[c];
-            s_G[c][hl] = hG[c];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            if (c < C) {
+                s_I[c][hl] = hI[c];
+                s_G[c][hl] = hG[c];
+            }
         }
     }
     __syncthreads();
@@ -792,14 +830,18 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
     if (inside && fi >= 0) {
         // Differentiation.backward at this pixel
         float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
-        for (int c = 0; c < C; c++) {
-            Im[c] = s_I[c][li - 1]; Ip[c] = s_I[c][li + 1];
-            Gm[c] = s_G[c][li - 1]; Gp[c] = s_G[c][li + 1];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            const bool u = c < C;
+            Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
+            Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
         }
         const float gx = axis_grad(Im, I, Ip, Gm, G, Gp, px, S, C, a.step);
-        for (int c = 0; c < C; c++) {
-            Im[c] = s_I[c][li - HW_]; Ip[c] = s_I[c][li + HW_];
-            Gm[c] = s_G[c][li - HW_]; Gp[c] = s_G[c][li + HW_];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            const bool u = c < C;
+            Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
+            Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
         }
         const float gy = axis_grad(Im, I, Ip, Gm, G, Gp, py, S, C, a.step);
 
@@ -807,6 +849,7 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         face_weights(xp, yp, f, w);
         // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
         float gF[9];
+        #pragma unroll
         for (int k = 0; k < 3; k++) {
             gF[3 * k + 0] = gx * w[k];
             gF[3 * k + 1] = gy * w[k];
@@ -822,9 +865,11 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
             c = 3;
             // bilinear: images = sum_i wt_i T_i  -> textures and weights
             float gw[4];
+            #pragma unroll
             for (int i = 0; i < 4; i++) {
                 float acc = 0.f;
                 float gt[3];
+                #pragma unroll
                 for (int ch = 0; ch < 3; ch++) {
                     const float tv = texel(sh.tv, bt, ch, s.idx[i]);
                     acc = (ch == 0) ? gc[ch] * tv : acc + gc[ch] * tv;
@@ -836,6 +881,7 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
                 } else if (a.grad_tex4 && (gt[0] != 0.f || gt[1] != 0.f || gt[2] != 0.f)) {
                     const int p = s.idx[i];
                     const int slot = lds_slot(s_tkey, TSLOTS - 1, p >> 2);
+                    #pragma unroll
                     for (int ch = 0; ch < 3; ch++) {
                         if (gt[ch] == 0.f) continue;
                         if (slot >= 0) atomicAdd(&s_tval[slot * 16 + (p & 3) * 4 + ch], gt[ch]);
@@ -854,6 +900,7 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
             g_y = g_y + gw[3] * bx;
             const float gp[2] = {g_x, g_y};
             float gpr[2];
+            #pragma unroll
             for (int j = 0; j < 2; j++) {
                 // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
                 const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
@@ -864,8 +911,10 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
             }
             const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
             const float g_st = -g_dt * (s.dt * s.dt);
+            #pragma unroll
             for (int k = 0; k < 3; k++) {
                 float gz = 0.f;
+                #pragma unroll
                 for (int j = 0; j < 2; j++) {
                     const float pk = w[k] * fuv[2 * k + j];
                     gz = gz + (-(gpr[j] * s.dt)) * ((pk / s.zq[k]) / s.zq[k]);
@@ -876,15 +925,18 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         }
         if (sh.draw & NR_DRAW_SILHOUETTES) c++;
         if (sh.draw & NR_DRAW_DEPTH) {
-            const float gd = G[c];
-            const float d = I[c];
+            const float gd = pick(G, c);
+            const float d = pick(I, c);
             const float g_s = -gd * (d * d);
+            #pragma unroll
             for (int k = 0; k < 3; k++) gF[3 * k + 2] += (-g_s) * ((w[k] / z[k]) / z[k]);
         }
         if (NR_ABLATE & 2) {
+            #pragma unroll
             for (int k = 0; k < 9; k++) asm volatile("" ::"v"(gF[k]));
         } else {
         const int slot = lds_slot(s_fkey, FSLOTS - 1, fi);
+        #pragma unroll
         for (int k = 0; k < 9; k++) {
             if (gF[k] == 0.f) continue;
             if (slot >= 0) atomicAdd(&s_fval[slot * 9 + k], gF[k]);
@@ -1027,7 +1079,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     FwdOut out;
     out.fim = fim;
     out.images = images;
-    dim3 grid(g.tiles_x * g.tiles_y, B);
+    dim3 grid(g.nbins, B);
     if (ra) {
         Shade sh = make_shade(ra);
         hipLaunchKernelGGL(k_raster_fwd<true>, grid, dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far, delta,

@@ -15,11 +15,12 @@
 //   k_raster_fwd     one block per 32x32-pixel coarse bin: stages the bin's candidate faces in face
 //                    order into LDS, each wave walks (ballot) the faces touching its pixels in order,
 //                    then shades rgb/sil/depth and writes fim + the flipped, 2x2-averaged output.
-//   backward         k_raster_bwd: one block per tile with a 1-pixel halo: recomputes the internal
+//   backward         k_raster_bwd: one block per 32x16 pixels + 1-pixel halo: recomputes the internal
 //                    image from fim, applies Differentiation.backward's stencil, and chains the
 //                    coordinate / depth / texture gradients to vertices and textures with atomics.
 #include <hip/hip_runtime.h>
 
+#include <limits.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -691,19 +692,23 @@ __global__ void k_diff_bwd(const float* __restrict__ img, const float* __restric
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_raster_bwd: per 32x8 tile with a 1-pixel halo.
-//   1. recompute the internal image I (all channels) and the upstream gradient G of the tile + halo
-//      into LDS (Differentiation saved images; the flip/AA backward is an index map + /4);
+// k_raster_bwd: one block per 32x16 pixels (2 pixels per thread: two 32x8 sub-tiles) + 1-pixel halo.
+//   1. recompute the internal image I (all channels) and the upstream gradient G of the block +
+//      halo into LDS (Differentiation saved the images; the flip/AA backward is an index map + /4);
 //   2. per foreground pixel: the soft-gradient stencil (gx, gy) and the chain rule through the
 //      coordinate, depth and texture maps;
-//   3. the per-pixel gradients are reduced in LDS hash tables keyed by face id (9 floats, the
-//      gathered-face gradient of rasterize.py:232) and by 64-byte texel segment (4 texels x RGBA),
-//      then flushed with global float atomics whose lanes cover whole records / whole 64-byte
-//      segments (MI355X float atomics are priced per 64-byte request).
-constexpr int HW_ = TW + 2, HH_ = TH + 2, HN = HW_ * HH_;
-constexpr int FSLOTS = 256;   // face table (one pixel -> one face: at most NT distinct)
-constexpr int TSLOTS = 256;   // texel-segment table; misses fall back to direct atomics
-constexpr int PROBES = 32;
+//   3. reduction: per wave and sub-tile, the lanes are grouped by face id (ballot match loop); one
+//      lane per distinct face inserts it into an LDS slot table, then every lane adds its 9 face
+//      gradients and its bilinear texture gradients into the slot (a 4x4-texel window per face:
+//      create_textures-style atlases; texels outside the window go straight to global atomics);
+//   4. flush: one global float atomic per nonzero value, lanes covering whole face records and whole
+//      4-texel RGBA rows (MI355X float atomics are priced per 64-byte request).
+constexpr int BH = 16;                        // block height (two 32x8 sub-tiles)
+constexpr int HW_ = TW + 2, HH_ = BH + 2, HN = HW_ * HH_;
+constexpr int NHALO = 2 * HW_ + 2 * BH;       // 100 halo pixels
+constexpr int FSLOTS = 64;                    // faces per block with LDS accumulators
+constexpr int TWIN = 4;                       // texel window edge per face slot
+constexpr int TWN = TWIN * TWIN * 3;          // floats per texel window
 // experiment switch for timing builds (never set in the shipped library):
 //   1 = no global flush of the LDS tables, 2 = no gradient accumulation at all
 #ifndef NR_ABLATE
@@ -734,82 +739,112 @@ __device__ __forceinline__ void upstream_grad(const BwdArgs& a, int C, int b, in
     }
 }
 
-// open-addressing slot of `key` in an LDS table of (mask + 1) slots, inserting it if absent;
-// -1 when PROBES slots are taken by other keys
-__device__ __forceinline__ int lds_slot(int* keys, int mask, int key) {
+__device__ __forceinline__ float upstream_one(const BwdArgs& a, int C, int b, int y, int x, int S, int c) {
+    if (a.aa) {
+        const int s = a.s;
+        return a.grad_images[(((long long)b * C + c) * s + ((S - 1 - y) >> 1)) * s + ((S - 1 - x) >> 1)] / 4.f;
+    }
+    return a.grad_images[(((long long)b * C + c) * S + (S - 1 - y)) * S + (S - 1 - x)];
+}
+
+// slot of `key` in an LDS table of FSLOTS, inserting it if absent; -1 when the table is full
+__device__ __forceinline__ int lds_slot(int* keys, int key, bool& inserted) {
     const unsigned h = ((unsigned)key * 2654435761u) >> 7;
-    for (int i = 0; i < PROBES; i++) {
-        const int sidx = (int)((h + i) & mask);
+    inserted = false;
+    for (int i = 0; i < FSLOTS; i++) {
+        const int sidx = (int)((h + i) & (FSLOTS - 1));
         const int k = __hip_atomic_load(&keys[sidx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (k == key) return sidx;
         if (k == -1) {
             const int old = atomicCAS(&keys[sidx], -1, key);
-            if (old == -1 || old == key) return sidx;
+            if (old == -1) {
+                inserted = true;
+                return sidx;
+            }
+            if (old == key) return sidx;
         }
     }
     return -1;
+}
+
+// texel window origin of a face (floor of its smallest u, v); invalid (INT_MIN) if not finite
+__device__ __forceinline__ int2 window_origin(const TexSample& s) {
+    const bool ok = fabsf(s.lo[0]) < 1e9f && fabsf(s.lo[1]) < 1e9f;
+    return ok ? make_int2((int)floorf(s.lo[0]), (int)floorf(s.lo[1])) : make_int2(INT_MIN, INT_MIN);
 }
 
 __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) {
     __shared__ float s_I[MAXC][HN];
     __shared__ float s_G[MAXC][HN];
     __shared__ int s_fkey[FSLOTS];
-    __shared__ __attribute__((aligned(16))) float s_fval[FSLOTS * 9];
-    __shared__ int s_tkey[TSLOTS];
-    __shared__ __attribute__((aligned(16))) float s_tval[TSLOTS * 16];
+    __shared__ int2 s_fwin[FSLOTS];
+    __shared__ float s_fval[FSLOTS * 9];
+    __shared__ float s_tval[FSLOTS * TWN];
     const int b = blockIdx.y;
     const int S = g.S;
     const int C = sh.C;
     const bool rgb = (sh.draw & NR_DRAW_RGB) != 0;
-    const int tx0 = (blockIdx.x % g.tiles_x) * TW;
-    const int ty0 = (blockIdx.x / g.tiles_x) * TH;
+    const int bxs = (S + TW - 1) / TW;
+    const int tx0 = (blockIdx.x % bxs) * TW;
+    const int ty0 = (blockIdx.x / bxs) * BH;
     const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int bt = sh.tv.sb ? b : 0;
 
-    // clear the tables
-    s_fkey[t] = -1;
-    s_tkey[t] = -1;
-    for (int i = t; i < FSLOTS * 9 / 4; i += NT) reinterpret_cast<float4*>(s_fval)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < FSLOTS) s_fkey[t] = -1;
+    for (int i = t; i < FSLOTS * 9; i += NT) s_fval[i] = 0.f;
     if (rgb)
-        for (int i = t; i < TSLOTS * 16 / 4; i += NT) reinterpret_cast<float4*>(s_tval)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = t; i < FSLOTS * TWN; i += NT) s_tval[i] = 0.f;
 
     int lx, ly;
     pixel_of(t, lx, ly);
-    const int px = tx0 + lx, py = ty0 + ly;
-    const bool inside = px < S && py < S;
-    const float xp = pix_center(px, S), yp = pix_center(py, S);
+    const int px = tx0 + lx;
+    const float xp = pix_center(px, S);
 
-    int fi = -1;
-    Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    float I[MAXC], G[MAXC];
-    #pragma unroll
-    for (int c = 0; c < MAXC; c++) I[c] = G[c] = 0.f;
-    if (inside) {
-        fi = a.fim[((long long)b * S + py) * S + px];
-        if (fi >= 0) f = load_face(a.face_records + ((long long)b * a.F + fi) * 9);
-        shade_pixel(sh, b, fi, f, xp, yp, I);
-        upstream_grad(a, C, b, py, px, S, G);
-    }
-    const int li = (ly + 1) * HW_ + (lx + 1);
+    // ---- 1. image and upstream gradient of the two interior pixels and one halo pixel ----------
+    int fi[2];
 #pragma unroll
-    for (int c = 0; c < MAXC; c++) {
-        if (c < C) {
-            s_I[c][li] = I[c];
-            s_G[c][li] = G[c];
-        }
+    for (int k = 0; k < 2; k++) {
+        const int py = ty0 + TH * k + ly;
+        fi[k] = (px < S && py < S) ? a.fim[((long long)b * S + py) * S + px] : -1;
     }
-    // halo ring: 2 rows of HW_ + 2 columns of TH
-    if (t < 2 * HW_ + 2 * TH) {
-        int hx, hy;
+    int hy = 0, hx = 0, hf = -1;
+    bool hin = false;
+    if (t < NHALO) {
         if (t < HW_) { hy = 0; hx = t; }
         else if (t < 2 * HW_) { hy = HH_ - 1; hx = t - HW_; }
-        else if (t < 2 * HW_ + TH) { hy = 1 + (t - 2 * HW_); hx = 0; }
-        else { hy = 1 + (t - 2 * HW_ - TH); hx = HW_ - 1; }
+        else if (t < 2 * HW_ + BH) { hy = 1 + (t - 2 * HW_); hx = 0; }
+        else { hy = 1 + (t - 2 * HW_ - BH); hx = HW_ - 1; }
+        const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+        hin = y >= 0 && y < S && x >= 0 && x < S;
+        hf = hin ? a.fim[((long long)b * S + y) * S + x] : -1;
+    }
+    float I2[2][MAXC], G2[2][MAXC];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int py = ty0 + TH * k + ly;
+        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (fi[k] >= 0) f = load_face(a.face_records + ((long long)b * a.F + fi[k]) * 9);
+        shade_pixel(sh, b, fi[k], f, xp, pix_center(py, S), I2[k]);
+        if (px < S && py < S) upstream_grad(a, C, b, py, px, S, G2[k]);
+        else
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) G2[k][c] = 0.f;
+        const int li = (ly + TH * k + 1) * HW_ + (lx + 1);
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            if (c < C) {
+                s_I[c][li] = I2[k][c];
+                s_G[c][li] = G2[k][c];
+            }
+        }
+    }
+    if (t < NHALO) {
         const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
         float hI[MAXC], hG[MAXC];
-        #pragma unroll
+#pragma unroll
         for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
-        if (y >= 0 && y < S && x >= 0 && x < S) {
-            const int hf = a.fim[((long long)b * S + y) * S + x];
+        if (hin) {
             Face ff = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             if (hf >= 0) ff = load_face(a.face_records + ((long long)b * a.F + hf) * 9);
             shade_pixel(sh, b, hf, ff, pix_center(x, S), pix_center(y, S), hI);
@@ -826,140 +861,189 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
     }
     __syncthreads();
 
-    const int bt = sh.tv.sb ? b : 0;
-    if (inside && fi >= 0) {
-        // Differentiation.backward at this pixel
-        float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) {
-            const bool u = c < C;
-            Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
-            Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
-        }
-        const float gx = axis_grad(Im, I, Ip, Gm, G, Gp, px, S, C, a.step);
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) {
-            const bool u = c < C;
-            Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
-            Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
-        }
-        const float gy = axis_grad(Im, I, Ip, Gm, G, Gp, py, S, C, a.step);
-
-        float w[3];
-        face_weights(xp, yp, f, w);
-        // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
+    // ---- 2./3. per sub-tile: gradients of my pixel, grouped by face across the wave -------------
+    auto sub_tile = [&](const int k, const int fik, const float (&I)[MAXC], const float (&G)[MAXC]) {
+        const int py = ty0 + TH * k + ly;
+        const float yp = pix_center(py, S);
+        const bool act = fik >= 0;  // implies inside the image
         float gF[9];
-        #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            gF[3 * k + 0] = gx * w[k];
-            gF[3 * k + 1] = gy * w[k];
-            gF[3 * k + 2] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 9; j++) gF[j] = 0.f;
+        int tx[4], ty[4], tidx[4];
+        float tg[4][3];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            tx[i] = ty[i] = tidx[i] = 0;
+            tg[i][0] = tg[i][1] = tg[i][2] = 0.f;
         }
-        const float z[3] = {f.z0, f.z1, f.z2};
-        int c = 0;
-        if (rgb) {
-            TexSample s;
-            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
-            sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
-            const float gc[3] = {G[0], G[1], G[2]};
-            c = 3;
-            // bilinear: images = sum_i wt_i T_i  -> textures and weights
-            float gw[4];
-            #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                float acc = 0.f;
-                float gt[3];
-                #pragma unroll
-                for (int ch = 0; ch < 3; ch++) {
-                    const float tv = texel(sh.tv, bt, ch, s.idx[i]);
-                    acc = (ch == 0) ? gc[ch] * tv : acc + gc[ch] * tv;
-                    gt[ch] = gc[ch] * s.wt[i];
-                }
-                gw[i] = acc;
-                if (NR_ABLATE & 2) {
-                    asm volatile("" ::"v"(gt[0]), "v"(gt[1]), "v"(gt[2]));
-                } else if (a.grad_tex4 && (gt[0] != 0.f || gt[1] != 0.f || gt[2] != 0.f)) {
-                    const int p = s.idx[i];
-                    const int slot = lds_slot(s_tkey, TSLOTS - 1, p >> 2);
-                    #pragma unroll
+        int2 win = make_int2(INT_MIN, INT_MIN);
+        if (act) {
+            const int li = (ly + TH * k + 1) * HW_ + (lx + 1);
+            // Differentiation.backward at this pixel
+            float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                const bool u = c < C;
+                Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
+                Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
+            }
+            const float gx = axis_grad(Im, I, Ip, Gm, G, Gp, px, S, C, a.step);
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                const bool u = c < C;
+                Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
+                Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
+            }
+            const float gy = axis_grad(Im, I, Ip, Gm, G, Gp, py, S, C, a.step);
+
+            const Face f = load_face(a.face_records + ((long long)b * a.F + fik) * 9);
+            float w[3];
+            face_weights(xp, yp, f, w);
+            // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                gF[3 * j + 0] = gx * w[j];
+                gF[3 * j + 1] = gy * w[j];
+            }
+            const float z[3] = {f.z0, f.z1, f.z2};
+            if (rgb) {
+                TexSample s;
+                const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fik * 6;
+                sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
+                win = window_origin(s);
+                // bilinear: images = sum_i wt_i T_i  -> textures and weights
+                float gw[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    float acc = 0.f;
+#pragma unroll
                     for (int ch = 0; ch < 3; ch++) {
-                        if (gt[ch] == 0.f) continue;
-                        if (slot >= 0) atomicAdd(&s_tval[slot * 16 + (p & 3) * 4 + ch], gt[ch]);
-                        else unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + p) * 4 + ch, gt[ch]);
+                        const float tv = texel(sh.tv, bt, ch, s.idx[i]);
+                        acc = (ch == 0) ? G[ch] * tv : acc + G[ch] * tv;
+                        tg[i][ch] = G[ch] * s.wt[i];
+                    }
+                    gw[i] = acc;
+                    tidx[i] = s.idx[i];
+                    tx[i] = (i & 1) ? (int)s.x1 : (int)s.x0;
+                    ty[i] = (i & 2) ? (int)s.y1 : (int)s.y0;
+                }
+                const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
+                float g_x = -(gw[0] * ay);
+                g_x = g_x + gw[1] * ay;
+                g_x = g_x - gw[2] * by;
+                g_x = g_x + gw[3] * by;
+                float g_y = -(gw[0] * ax);
+                g_y = g_y - gw[1] * bx;
+                g_y = g_y + gw[2] * ax;
+                g_y = g_y + gw[3] * bx;
+                const float gp[2] = {g_x, g_y};
+                float gpr[2];
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
+                    const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
+                    float gg = gp[j];
+                    gg = (pc == hm) ? gg / 2 : (pc > hm ? 0.f : gg);
+                    gg = (pr == lo) ? gg / 2 : (pr < lo ? 0.f : gg);
+                    gpr[j] = gg;
+                }
+                const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
+                const float g_st = -g_dt * (s.dt * s.dt);
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    float gz = 0.f;
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const float pk = w[j] * fuv[2 * j + q];
+                        gz = gz + (-(gpr[q] * s.dt)) * ((pk / s.zq[j]) / s.zq[j]);
+                    }
+                    gz = gz + (-g_st) * ((w[j] / s.zq[j]) / s.zq[j]);
+                    gF[3 * j + 2] += gz;
+                }
+            }
+            if (sh.draw & NR_DRAW_DEPTH) {
+                // depth channel: its upstream gradient reloaded (a cache hit) and its value recomputed,
+                // rather than a runtime-indexed register array (which the compiler puts in scratch)
+                const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
+                const float gd = upstream_one(a, C, b, py, px, S, dc);
+                const float d = depth_value(f, w);
+                const float g_s = -gd * (d * d);
+#pragma unroll
+                for (int j = 0; j < 3; j++) gF[3 * j + 2] += (-g_s) * ((w[j] / z[j]) / z[j]);
+            }
+        }
+        if (NR_ABLATE & 2) {
+#pragma unroll
+            for (int j = 0; j < 9; j++) asm volatile("" ::"v"(gF[j]));
+#pragma unroll
+            for (int i = 0; i < 4; i++) asm volatile("" ::"v"(tg[i][0]), "v"(tg[i][1]), "v"(tg[i][2]));
+            return;
+        }
+        // group the wave's lanes by face: one slot lookup per distinct face
+        int slot = -1;
+        for (unsigned long long pending = __ballot(act); pending;) {
+            const int leader = __builtin_ctzll(pending);
+            const int key = __builtin_amdgcn_readlane(fik, leader);
+            const unsigned long long m = __ballot(act && fik == key);
+            int sl = -1;
+            if (lane == leader) {
+                bool ins;
+                sl = lds_slot(s_fkey, key, ins);
+                if (ins) s_fwin[sl] = win;
+            }
+            sl = __builtin_amdgcn_readlane(sl, leader);
+            if ((m >> lane) & 1ull) slot = sl;
+            pending &= ~m;
+        }
+        if (act) {
+            float* gfg = a.grad_faces + ((long long)b * a.F + fik) * 9;
+#pragma unroll
+            for (int j = 0; j < 9; j++) {
+                if (gF[j] == 0.f) continue;
+                if (slot >= 0) atomicAdd(&s_fval[slot * 9 + j], gF[j]);
+                else unsafeAtomicAdd(gfg + j, gF[j]);
+            }
+            if (rgb && a.grad_tex4) {
+                const bool wok = slot >= 0 && win.x != INT_MIN;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if (tg[i][0] == 0.f && tg[i][1] == 0.f && tg[i][2] == 0.f) continue;
+                    const int dx = tx[i] - win.x, dy = ty[i] - win.y;
+                    const bool inwin = wok && dx >= 0 && dx < TWIN && dy >= 0 && dy < TWIN && tx[i] >= 0 &&
+                                       ty[i] >= 0 && tx[i] < sh.tv.W && ty[i] < sh.tv.H;
+                    float* gtg = a.grad_tex4 + ((long long)bt * a.HWp + tidx[i]) * 4;
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) {
+                        if (tg[i][ch] == 0.f) continue;
+                        if (inwin) atomicAdd(&s_tval[slot * TWN + (dy * TWIN + dx) * 3 + ch], tg[i][ch]);
+                        else unsafeAtomicAdd(gtg + ch, tg[i][ch]);
                     }
                 }
             }
-            const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
-            float g_x = -(gw[0] * ay);
-            g_x = g_x + gw[1] * ay;
-            g_x = g_x - gw[2] * by;
-            g_x = g_x + gw[3] * by;
-            float g_y = -(gw[0] * ax);
-            g_y = g_y - gw[1] * bx;
-            g_y = g_y + gw[2] * ax;
-            g_y = g_y + gw[3] * bx;
-            const float gp[2] = {g_x, g_y};
-            float gpr[2];
-            #pragma unroll
-            for (int j = 0; j < 2; j++) {
-                // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
-                const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
-                float gg = gp[j];
-                gg = (pc == hm) ? gg / 2 : (pc > hm ? 0.f : gg);
-                gg = (pr == lo) ? gg / 2 : (pr < lo ? 0.f : gg);
-                gpr[j] = gg;
-            }
-            const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
-            const float g_st = -g_dt * (s.dt * s.dt);
-            #pragma unroll
-            for (int k = 0; k < 3; k++) {
-                float gz = 0.f;
-                #pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    const float pk = w[k] * fuv[2 * k + j];
-                    gz = gz + (-(gpr[j] * s.dt)) * ((pk / s.zq[k]) / s.zq[k]);
-                }
-                gz = gz + (-g_st) * ((w[k] / s.zq[k]) / s.zq[k]);
-                gF[3 * k + 2] += gz;
-            }
         }
-        if (sh.draw & NR_DRAW_SILHOUETTES) c++;
-        if (sh.draw & NR_DRAW_DEPTH) {
-            const float gd = pick(G, c);
-            const float d = pick(I, c);
-            const float g_s = -gd * (d * d);
-            #pragma unroll
-            for (int k = 0; k < 3; k++) gF[3 * k + 2] += (-g_s) * ((w[k] / z[k]) / z[k]);
-        }
-        if (NR_ABLATE & 2) {
-            #pragma unroll
-            for (int k = 0; k < 9; k++) asm volatile("" ::"v"(gF[k]));
-        } else {
-        const int slot = lds_slot(s_fkey, FSLOTS - 1, fi);
-        #pragma unroll
-        for (int k = 0; k < 9; k++) {
-            if (gF[k] == 0.f) continue;
-            if (slot >= 0) atomicAdd(&s_fval[slot * 9 + k], gF[k]);
-            else unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + fi) * 9 + k, gF[k]);
-        }
-        }
-    }
+    };
+    sub_tile(0, fi[0], I2[0], G2[0]);
+    sub_tile(1, fi[1], I2[1], G2[1]);
     __syncthreads();
     if (NR_ABLATE & 3) return;
-    // flush: consecutive lanes cover one record / one 64-byte texel segment
+    // ---- 4. flush: lanes cover whole 9-float face records / whole 4-texel RGBA rows -------------
     for (int e = t; e < FSLOTS * 9; e += NT) {
-        const int sl = e / 9, k = e - sl * 9;
+        const int sl = e / 9, j = e - sl * 9;
         const int key = s_fkey[sl];
         if (key < 0) continue;
         const float v = s_fval[e];
-        if (v != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + k, v);
+        if (v != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + j, v);
     }
     if (rgb && a.grad_tex4) {
-        for (int e = t; e < TSLOTS * 16; e += NT) {
-            const int key = s_tkey[e >> 4];
-            if (key < 0) continue;
-            const float v = s_tval[e];
-            if (v != 0.f) unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)key * 4) * 4 + (e & 15), v);
+        const int W = sh.tv.W, H = sh.tv.H;
+        for (int e = t; e < FSLOTS * TWIN * TWIN * 4; e += NT) {
+            const int sl = e >> 6, r = e & 63, tex = r >> 2, ch = r & 3;
+            if (ch == 3 || s_fkey[sl] < 0) continue;
+            const int2 wv = s_fwin[sl];
+            const float v = s_tval[sl * TWN + tex * 3 + ch];
+            if (v == 0.f) continue;
+            const int x = wv.x + (tex & (TWIN - 1)), y = wv.y + tex / TWIN;
+            if (x < W && y < H) unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)y * W + x) * 4 + ch, v);
         }
     }
 }
@@ -1191,7 +1275,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.HWp = HWp;
     ba.step = (float)(2. / S);
     Shade sh = make_shade(a);
-    hipLaunchKernelGGL(k_raster_bwd, dim3(g.tiles_x * g.tiles_y, a->batch_size), dim3(NT), 0, st, ba, g, sh);
+    hipLaunchKernelGGL(k_raster_bwd, dim3(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size), dim3(NT), 0, st, ba,
+                       g, sh);
     e = check_launch("k_raster_bwd");
     if (e) return e;
     const long long nv = (long long)a->batch_size * a->num_vertices;

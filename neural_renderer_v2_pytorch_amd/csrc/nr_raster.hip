@@ -692,25 +692,32 @@ __global__ void k_diff_bwd(const float* __restrict__ img, const float* __restric
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_raster_bwd: one block per 32x16 pixels (2 pixels per thread: two 32x8 sub-tiles) + 1-pixel halo.
-//   1. recompute the internal image I (all channels) and the upstream gradient G of the block +
-//      halo into LDS (Differentiation saved the images; the flip/AA backward is an index map + /4);
-//   2. per foreground pixel: the soft-gradient stencil (gx, gy) and the chain rule through the
-//      coordinate, depth and texture maps;
-//   3. reduction: per wave and sub-tile, the lanes are grouped by face id (ballot match loop); one
-//      lane per distinct face inserts it into an LDS slot table, then every lane adds its 9 face
-//      gradients and its bilinear texture gradients into the slot (a 4x4-texel window per face:
-//      create_textures-style atlases; texels outside the window go straight to global atomics);
-//   4. flush: one global float atomic per nonzero value, lanes covering whole face records and whole
-//      4-texel RGBA rows (MI355X float atomics are priced per 64-byte request).
-constexpr int BH = 16;                        // block height (two 32x8 sub-tiles)
+// k_raster_bwd: one block per 32x16 pixels + 1-pixel halo; each wave owns a 16x8 block, 2 pixels per
+// lane.
+//   1. recompute the internal image I (all channels, bit-identical to the forward) and the upstream
+//      gradient G of the block + halo into LDS (Differentiation saved the images; the flip/AA
+//      backward is an index map and /4), and for the block's own pixels the gradient terms that do
+//      not depend on the stencil (depth and texture-coordinate paths to z, bilinear weights);
+//   2. the soft-gradient stencil (gx, gy) of Differentiation.backward, then the coordinate-map chain
+//      rule -> a 9-float gradient of the gathered face (rasterize.py:232);
+//   3. reduction without LDS float atomics (ds_add_f32 runs at ~3 cycles per lane on gfx950,
+//      tools/ubench_lds_atomics.hip): each lane stages its two pixel records in LDS; the wave groups
+//      its records by face (ballot match loop); for each face, lanes 0..47 own the 4x4 texel x RGB
+//      window of the face and lanes 48..56 its 9 gradient floats, and sum over the face's records;
+//   4. one global float atomic per lane and face: a whole face record and whole 4-texel RGBA rows,
+//      i.e. a handful of 64-byte requests per (face, wave).
+//   Texel contributions outside a face's 4x4 window (atlases with larger per-face texture regions)
+//   go straight to global atomics in step 1.
+constexpr int BH = 16;                        // block height
 constexpr int HW_ = TW + 2, HH_ = BH + 2, HN = HW_ * HH_;
 constexpr int NHALO = 2 * HW_ + 2 * BH;       // 100 halo pixels
-constexpr int FSLOTS = 64;                    // faces per block with LDS accumulators
-constexpr int TWIN = 4;                       // texel window edge per face slot
-constexpr int TWN = TWIN * TWIN * 3;          // floats per texel window
+constexpr int TWIN = 4;                       // texel window edge per face
+constexpr int REC = 17;                       // staged record: gF[9] G_rgb[3] ay by ax bx pos
+constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
+constexpr int BWD_LDS_REC = 4 * 128 * REC * 4;
+constexpr int BWD_LDS = BWD_LDS_IG > BWD_LDS_REC ? BWD_LDS_IG : BWD_LDS_REC;
 // experiment switch for timing builds (never set in the shipped library):
-//   1 = no global flush of the LDS tables, 2 = no gradient accumulation at all
+//   2 = no gradient accumulation (steps 3 and 4)
 #ifndef NR_ABLATE
 #define NR_ABLATE 0
 #endif
@@ -722,7 +729,8 @@ struct BwdArgs {
     float* __restrict__ grad_faces;   // [B, F, 9]
     float* __restrict__ grad_tex4;    // [Bt, HWp, 4] or null
     int F, aa, s, HWp;
-    float step;
+    float step, inv_step;
+    int step_pow2;                     // x / step == x * inv_step exactly
 };
 
 __device__ __forceinline__ void upstream_grad(const BwdArgs& a, int C, int b, int y, int x, int S, float* G) {
@@ -747,90 +755,199 @@ __device__ __forceinline__ float upstream_one(const BwdArgs& a, int C, int b, in
     return a.grad_images[(((long long)b * C + c) * S + (S - 1 - y)) * S + (S - 1 - x)];
 }
 
-// slot of `key` in an LDS table of FSLOTS, inserting it if absent; -1 when the table is full
-__device__ __forceinline__ int lds_slot(int* keys, int key, bool& inserted) {
-    const unsigned h = ((unsigned)key * 2654435761u) >> 7;
-    inserted = false;
-    for (int i = 0; i < FSLOTS; i++) {
-        const int sidx = (int)((h + i) & (FSLOTS - 1));
-        const int k = __hip_atomic_load(&keys[sidx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (k == key) return sidx;
-        if (k == -1) {
-            const int old = atomicCAS(&keys[sidx], -1, key);
-            if (old == -1) {
-                inserted = true;
-                return sidx;
-            }
-            if (old == key) return sidx;
-        }
-    }
-    return -1;
+__device__ __forceinline__ float div_step(const BwdArgs& a, float x) { return a.step_pow2 ? x * a.inv_step : x / a.step; }
+
+__device__ __forceinline__ float stencil(const BwdArgs& a, const float* Im, const float* I0, const float* Ip,
+                                         const float* Gm, const float* G0, const float* Gp, int i, int n, int C) {
+    const bool has_p = i <= n - 2, has_m = i >= 1;
+    const float r_i = has_p ? div_step(a, -pair_dot(I0, Ip, Gp, C)) : 0.f;
+    const float r_m = has_m ? div_step(a, -pair_dot(Im, I0, G0, C)) : 0.f;
+    const float l_i = has_p ? div_step(a, -pair_dot(Ip, I0, G0, C)) : 0.f;
+    const float l_m = has_m ? div_step(a, -pair_dot(I0, Im, Gm, C)) : 0.f;
+    return pick_grad(r_i + r_m, l_m + l_i);
 }
 
-// texel window origin of a face (floor of its smallest u, v); invalid (INT_MIN) if not finite
-__device__ __forceinline__ int2 window_origin(const TexSample& s) {
-    const bool ok = fabsf(s.lo[0]) < 1e9f && fabsf(s.lo[1]) < 1e9f;
-    return ok ? make_int2((int)floorf(s.lo[0]), (int)floorf(s.lo[1])) : make_int2(INT_MIN, INT_MIN);
-}
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// per interior pixel state carried across the stencil's barrier
+struct BwdPix {
+    int fi;            // face index (-1: background or outside)
+    float w[3];        // barycentric weights (compute_weight_map)
+    float gz[3];       // d/dz of the face corners through the depth and texture-coordinate paths
+    float grgb[3];     // upstream gradient of the rgb channels
+    float ay, by, ax, bx;
+    int pos;           // bilinear top-left texel relative to the face window: dx | dy << 8; -1 none
+    int wx, wy;        // face window origin (texels); INT_MIN when not windowed
+};
 
 __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) {
-    __shared__ float s_I[MAXC][HN];
-    __shared__ float s_G[MAXC][HN];
-    __shared__ int s_fkey[FSLOTS];
-    __shared__ int2 s_fwin[FSLOTS];
-    __shared__ float s_fval[FSLOTS * 9];
-    __shared__ float s_tval[FSLOTS * TWN];
+    __shared__ __attribute__((aligned(16))) float s_raw[BWD_LDS / 4];
+    float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
+    float(*s_G)[HN] = reinterpret_cast<float(*)[HN]>(s_raw + MAXC * HN);
     const int b = blockIdx.y;
     const int S = g.S;
     const int C = sh.C;
     const bool rgb = (sh.draw & NR_DRAW_RGB) != 0;
+    const bool want_tex = rgb && a.grad_tex4 != nullptr;
     const int bxs = (S + TW - 1) / TW;
     const int tx0 = (blockIdx.x % bxs) * TW;
     const int ty0 = (blockIdx.x / bxs) * BH;
     const int t = threadIdx.x;
-    const int lane = t & 63;
+    const int lane = t & 63, wid = t >> 6;
     const int bt = sh.tv.sb ? b : 0;
-
-    if (t < FSLOTS) s_fkey[t] = -1;
-    for (int i = t; i < FSLOTS * 9; i += NT) s_fval[i] = 0.f;
-    if (rgb)
-        for (int i = t; i < FSLOTS * TWN; i += NT) s_tval[i] = 0.f;
-
-    int lx, ly;
-    pixel_of(t, lx, ly);
+    // wave wid owns the 16x8 block at (16 (wid & 1), 8 (wid >> 1)); lane -> column lane & 15, rows lane >> 4 (+4)
+    const int lx = (wid & 1) * 16 + (lane & 15);
+    const int ly0 = (wid >> 1) * 8 + (lane >> 4);
     const int px = tx0 + lx;
     const float xp = pix_center(px, S);
 
-    // ---- 1. image and upstream gradient of the two interior pixels and one halo pixel ----------
-    int fi[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int py = ty0 + TH * k + ly;
-        fi[k] = (px < S && py < S) ? a.fim[((long long)b * S + py) * S + px] : -1;
-    }
-    int hy = 0, hx = 0, hf = -1;
-    bool hin = false;
-    if (t < NHALO) {
-        if (t < HW_) { hy = 0; hx = t; }
-        else if (t < 2 * HW_) { hy = HH_ - 1; hx = t - HW_; }
-        else if (t < 2 * HW_ + BH) { hy = 1 + (t - 2 * HW_); hx = 0; }
-        else { hy = 1 + (t - 2 * HW_ - BH); hx = HW_ - 1; }
-        const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
-        hin = y >= 0 && y < S && x >= 0 && x < S;
-        hf = hin ? a.fim[((long long)b * S + y) * S + x] : -1;
-    }
+    // ---- 1. image + upstream gradient (LDS), and the stencil-independent gradient terms ---------
+    BwdPix P[2];
     float I2[2][MAXC], G2[2][MAXC];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-        const int py = ty0 + TH * k + ly;
-        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (fi[k] >= 0) f = load_face(a.face_records + ((long long)b * a.F + fi[k]) * 9);
-        shade_pixel(sh, b, fi[k], f, xp, pix_center(py, S), I2[k]);
-        if (px < S && py < S) upstream_grad(a, C, b, py, px, S, G2[k]);
-        else
+        const int py = ty0 + ly0 + 4 * k;
+        const bool inside = px < S && py < S;
+        BwdPix& q = P[k];
+        q.fi = inside ? a.fim[((long long)b * S + py) * S + px] : -1;
+        q.pos = -1;
+        q.wx = q.wy = INT_MIN;
+        q.w[0] = q.w[1] = q.w[2] = 0.f;
+        q.gz[0] = q.gz[1] = q.gz[2] = 0.f;
+        q.grgb[0] = q.grgb[1] = q.grgb[2] = 0.f;
+        q.ay = q.by = q.ax = q.bx = 0.f;
 #pragma unroll
-            for (int c = 0; c < MAXC; c++) G2[k][c] = 0.f;
-        const int li = (ly + TH * k + 1) * HW_ + (lx + 1);
+        for (int c = 0; c < MAXC; c++) I2[k][c] = G2[k][c] = 0.f;
+        if (inside) upstream_grad(a, C, b, py, px, S, G2[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int py = ty0 + ly0 + 4 * k;
+        BwdPix& q = P[k];
+        if (q.fi < 0) continue;
+        const float yp = pix_center(py, S);
+        const float* G = G2[k];
+        const Face f = load_face(a.face_records + ((long long)b * a.F + q.fi) * 9);
+        face_weights(xp, yp, f, q.w);
+        const float* w = q.w;
+        float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
+        if (rgb) {
+            TexSample s;
+            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)q.fi * 6;
+            sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
+            r = s.rgb[0];
+            gg = s.rgb[1];
+            bb = s.rgb[2];
+            // bilinear: images = sum_i wt_i T_i -> textures (staged below) and weights
+            float gw[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                float acc = 0.f;
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) {
+                    const float tv = texel(sh.tv, bt, ch, s.idx[i]);
+                    acc = (ch == 0) ? G[ch] * tv : acc + G[ch] * tv;
+                }
+                gw[i] = acc;
+            }
+            q.ay = s.y1 - s.y;
+            q.by = s.y - s.y0;
+            q.ax = s.x1 - s.x;
+            q.bx = s.x - s.x0;
+            q.grgb[0] = G[0];
+            q.grgb[1] = G[1];
+            q.grgb[2] = G[2];
+            if (want_tex) {
+                const bool wok = fabsf(s.lo[0]) < 1e9f && fabsf(s.lo[1]) < 1e9f;
+                const int ix0 = (int)s.x0, iy0 = (int)s.y0;
+                if (wok) {
+                    q.wx = (int)floorf(s.lo[0]);
+                    q.wy = (int)floorf(s.lo[1]);
+                }
+                const int dx = ix0 - q.wx, dy = iy0 - q.wy;
+                // corners with nonzero weight inside the window and the texture (no row wrap)
+                bool fits = wok;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float wt = ((i & 2) ? q.by : q.ay) * ((i & 1) ? q.bx : q.ax);
+                    if (wt == 0.f) continue;
+                    const int cx = dx + (i & 1), cy = dy + (i >> 1);
+                    const int gx_ = ix0 + (i & 1), gy_ = iy0 + (i >> 1);
+                    fits = fits && cx >= 0 && cx < TWIN && cy >= 0 && cy < TWIN && gx_ >= 0 && gy_ >= 0 &&
+                           gx_ < sh.tv.W && gy_ < sh.tv.H;
+                }
+                if (fits) {
+                    q.pos = dx | (dy << 8);
+                } else {
+                    // outside the face window: direct atomics (texel index as sampled)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        float* gtg = a.grad_tex4 + ((long long)bt * a.HWp + s.idx[i]) * 4;
+#pragma unroll
+                        for (int ch = 0; ch < 3; ch++) {
+                            const float v = G[ch] * s.wt[i];
+                            if (v != 0.f) unsafeAtomicAdd(gtg + ch, v);
+                        }
+                    }
+                }
+            }
+            // texture coordinates -> z (gradient-only terms: reciprocal multiplies)
+            const float ayv = q.ay, byv = q.by, axv = q.ax, bxv = q.bx;
+            float g_x = -(gw[0] * ayv);
+            g_x = g_x + gw[1] * ayv;
+            g_x = g_x - gw[2] * byv;
+            g_x = g_x + gw[3] * byv;
+            float g_y = -(gw[0] * axv);
+            g_y = g_y - gw[1] * bxv;
+            g_y = g_y + gw[2] * axv;
+            g_y = g_y + gw[3] * bxv;
+            const float gp[2] = {g_x, g_y};
+            float gpr[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
+                const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
+                float gq = gp[j];
+                gq = (pc == hm) ? gq * 0.5f : (pc > hm ? 0.f : gq);
+                gq = (pr == lo) ? gq * 0.5f : (pr < lo ? 0.f : gq);
+                gpr[j] = gq;
+            }
+            const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
+            const float g_st = -g_dt * (s.dt * s.dt);
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const float rz = frcp(s.zq[j]);
+                float gzj = 0.f;
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) gzj += (-(gpr[qq] * s.dt)) * (w[j] * fuv[2 * j + qq]) * rz * rz;
+                gzj += (-g_st) * w[j] * rz * rz;
+                q.gz[j] = gzj;
+            }
+        }
+        if (sh.draw & NR_DRAW_DEPTH) {
+            dep = depth_value(f, w);
+            // depth channel gradient reloaded (cache hit) rather than a runtime-indexed register array
+            const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
+            const float gd = upstream_one(a, C, b, py, px, S, dc);
+            const float g_s = -gd * (dep * dep);
+            const float z[3] = {f.z0, f.z1, f.z2};
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const float rz = frcp(z[j]);
+                q.gz[j] += (-g_s) * w[j] * rz * rz;
+            }
+        }
+        // channel values in merge order (rgb, sil, depth), compile-time slots as in shade_pixel
+        const bool R = rgb, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
+        I2[k][0] = R ? r : (Sl ? 1.f : dep);
+        I2[k][1] = R ? gg : dep;
+        I2[k][2] = bb;
+        I2[k][3] = Sl ? 1.f : dep;
+        I2[k][4] = dep;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
             if (c < C) {
@@ -839,12 +956,19 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
             }
         }
     }
+    // halo ring: image and upstream gradient only
     if (t < NHALO) {
+        int hy, hx;
+        if (t < HW_) { hy = 0; hx = t; }
+        else if (t < 2 * HW_) { hy = HH_ - 1; hx = t - HW_; }
+        else if (t < 2 * HW_ + BH) { hy = 1 + (t - 2 * HW_); hx = 0; }
+        else { hy = 1 + (t - 2 * HW_ - BH); hx = HW_ - 1; }
         const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
         float hI[MAXC], hG[MAXC];
 #pragma unroll
         for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
-        if (hin) {
+        if (y >= 0 && y < S && x >= 0 && x < S) {
+            const int hf = a.fim[((long long)b * S + y) * S + x];
             Face ff = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             if (hf >= 0) ff = load_face(a.face_records + ((long long)b * a.F + hf) * 9);
             shade_pixel(sh, b, hf, ff, pix_center(x, S), pix_center(y, S), hI);
@@ -861,189 +985,101 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
     }
     __syncthreads();
 
-    // ---- 2./3. per sub-tile: gradients of my pixel, grouped by face across the wave -------------
-    auto sub_tile = [&](const int k, const int fik, const float (&I)[MAXC], const float (&G)[MAXC]) {
-        const int py = ty0 + TH * k + ly;
-        const float yp = pix_center(py, S);
-        const bool act = fik >= 0;  // implies inside the image
-        float gF[9];
+    // ---- 2. Differentiation.backward stencil -> coordinate-map gradient ------------------------
+    float gF[2][9];
 #pragma unroll
-        for (int j = 0; j < 9; j++) gF[j] = 0.f;
-        int tx[4], ty[4], tidx[4];
-        float tg[4][3];
+    for (int k = 0; k < 2; k++) {
+        const BwdPix& q = P[k];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            tx[i] = ty[i] = tidx[i] = 0;
-            tg[i][0] = tg[i][1] = tg[i][2] = 0.f;
+        for (int j = 0; j < 9; j++) gF[k][j] = 0.f;
+        if (q.fi < 0) continue;
+        const int py = ty0 + ly0 + 4 * k;
+        const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
+        float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            const bool u = c < C;
+            Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
+            Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
         }
-        int2 win = make_int2(INT_MIN, INT_MIN);
-        if (act) {
-            const int li = (ly + TH * k + 1) * HW_ + (lx + 1);
-            // Differentiation.backward at this pixel
-            float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
+        const float gx = stencil(a, Im, I2[k], Ip, Gm, G2[k], Gp, px, S, C);
 #pragma unroll
-            for (int c = 0; c < MAXC; c++) {
-                const bool u = c < C;
-                Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
-                Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
-            }
-            const float gx = axis_grad(Im, I, Ip, Gm, G, Gp, px, S, C, a.step);
-#pragma unroll
-            for (int c = 0; c < MAXC; c++) {
-                const bool u = c < C;
-                Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
-                Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
-            }
-            const float gy = axis_grad(Im, I, Ip, Gm, G, Gp, py, S, C, a.step);
-
-            const Face f = load_face(a.face_records + ((long long)b * a.F + fik) * 9);
-            float w[3];
-            face_weights(xp, yp, f, w);
-            // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                gF[3 * j + 0] = gx * w[j];
-                gF[3 * j + 1] = gy * w[j];
-            }
-            const float z[3] = {f.z0, f.z1, f.z2};
-            if (rgb) {
-                TexSample s;
-                const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fik * 6;
-                sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
-                win = window_origin(s);
-                // bilinear: images = sum_i wt_i T_i  -> textures and weights
-                float gw[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    float acc = 0.f;
-#pragma unroll
-                    for (int ch = 0; ch < 3; ch++) {
-                        const float tv = texel(sh.tv, bt, ch, s.idx[i]);
-                        acc = (ch == 0) ? G[ch] * tv : acc + G[ch] * tv;
-                        tg[i][ch] = G[ch] * s.wt[i];
-                    }
-                    gw[i] = acc;
-                    tidx[i] = s.idx[i];
-                    tx[i] = (i & 1) ? (int)s.x1 : (int)s.x0;
-                    ty[i] = (i & 2) ? (int)s.y1 : (int)s.y0;
-                }
-                const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
-                float g_x = -(gw[0] * ay);
-                g_x = g_x + gw[1] * ay;
-                g_x = g_x - gw[2] * by;
-                g_x = g_x + gw[3] * by;
-                float g_y = -(gw[0] * ax);
-                g_y = g_y - gw[1] * bx;
-                g_y = g_y + gw[2] * ax;
-                g_y = g_y + gw[3] * bx;
-                const float gp[2] = {g_x, g_y};
-                float gpr[2];
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
-                    const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
-                    float gg = gp[j];
-                    gg = (pc == hm) ? gg / 2 : (pc > hm ? 0.f : gg);
-                    gg = (pr == lo) ? gg / 2 : (pr < lo ? 0.f : gg);
-                    gpr[j] = gg;
-                }
-                const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
-                const float g_st = -g_dt * (s.dt * s.dt);
-#pragma unroll
-                for (int j = 0; j < 3; j++) {
-                    float gz = 0.f;
-#pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        const float pk = w[j] * fuv[2 * j + q];
-                        gz = gz + (-(gpr[q] * s.dt)) * ((pk / s.zq[j]) / s.zq[j]);
-                    }
-                    gz = gz + (-g_st) * ((w[j] / s.zq[j]) / s.zq[j]);
-                    gF[3 * j + 2] += gz;
-                }
-            }
-            if (sh.draw & NR_DRAW_DEPTH) {
-                // depth channel: its upstream gradient reloaded (a cache hit) and its value recomputed,
-                // rather than a runtime-indexed register array (which the compiler puts in scratch)
-                const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
-                const float gd = upstream_one(a, C, b, py, px, S, dc);
-                const float d = depth_value(f, w);
-                const float g_s = -gd * (d * d);
-#pragma unroll
-                for (int j = 0; j < 3; j++) gF[3 * j + 2] += (-g_s) * ((w[j] / z[j]) / z[j]);
-            }
+        for (int c = 0; c < MAXC; c++) {
+            const bool u = c < C;
+            Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
+            Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
         }
-        if (NR_ABLATE & 2) {
+        const float gy = stencil(a, Im, I2[k], Ip, Gm, G2[k], Gp, py, S, C);
+        // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
 #pragma unroll
-            for (int j = 0; j < 9; j++) asm volatile("" ::"v"(gF[j]));
-#pragma unroll
-            for (int i = 0; i < 4; i++) asm volatile("" ::"v"(tg[i][0]), "v"(tg[i][1]), "v"(tg[i][2]));
-            return;
+        for (int j = 0; j < 3; j++) {
+            gF[k][3 * j + 0] = gx * q.w[j];
+            gF[k][3 * j + 1] = gy * q.w[j];
+            gF[k][3 * j + 2] = q.gz[j];
         }
-        // group the wave's lanes by face: one slot lookup per distinct face
-        int slot = -1;
-        for (unsigned long long pending = __ballot(act); pending;) {
-            const int leader = __builtin_ctzll(pending);
-            const int key = __builtin_amdgcn_readlane(fik, leader);
-            const unsigned long long m = __ballot(act && fik == key);
-            int sl = -1;
-            if (lane == leader) {
-                bool ins;
-                sl = lds_slot(s_fkey, key, ins);
-                if (ins) s_fwin[sl] = win;
-            }
-            sl = __builtin_amdgcn_readlane(sl, leader);
-            if ((m >> lane) & 1ull) slot = sl;
-            pending &= ~m;
-        }
-        if (act) {
-            float* gfg = a.grad_faces + ((long long)b * a.F + fik) * 9;
-#pragma unroll
-            for (int j = 0; j < 9; j++) {
-                if (gF[j] == 0.f) continue;
-                if (slot >= 0) atomicAdd(&s_fval[slot * 9 + j], gF[j]);
-                else unsafeAtomicAdd(gfg + j, gF[j]);
-            }
-            if (rgb && a.grad_tex4) {
-                const bool wok = slot >= 0 && win.x != INT_MIN;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if (tg[i][0] == 0.f && tg[i][1] == 0.f && tg[i][2] == 0.f) continue;
-                    const int dx = tx[i] - win.x, dy = ty[i] - win.y;
-                    const bool inwin = wok && dx >= 0 && dx < TWIN && dy >= 0 && dy < TWIN && tx[i] >= 0 &&
-                                       ty[i] >= 0 && tx[i] < sh.tv.W && ty[i] < sh.tv.H;
-                    float* gtg = a.grad_tex4 + ((long long)bt * a.HWp + tidx[i]) * 4;
-#pragma unroll
-                    for (int ch = 0; ch < 3; ch++) {
-                        if (tg[i][ch] == 0.f) continue;
-                        if (inwin) atomicAdd(&s_tval[slot * TWN + (dy * TWIN + dx) * 3 + ch], tg[i][ch]);
-                        else unsafeAtomicAdd(gtg + ch, tg[i][ch]);
-                    }
-                }
-            }
-        }
-    };
-    sub_tile(0, fi[0], I2[0], G2[0]);
-    sub_tile(1, fi[1], I2[1], G2[1]);
-    __syncthreads();
-    if (NR_ABLATE & 3) return;
-    // ---- 4. flush: lanes cover whole 9-float face records / whole 4-texel RGBA rows -------------
-    for (int e = t; e < FSLOTS * 9; e += NT) {
-        const int sl = e / 9, j = e - sl * 9;
-        const int key = s_fkey[sl];
-        if (key < 0) continue;
-        const float v = s_fval[e];
-        if (v != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + j, v);
     }
-    if (rgb && a.grad_tex4) {
-        const int W = sh.tv.W, H = sh.tv.H;
-        for (int e = t; e < FSLOTS * TWIN * TWIN * 4; e += NT) {
-            const int sl = e >> 6, r = e & 63, tex = r >> 2, ch = r & 3;
-            if (ch == 3 || s_fkey[sl] < 0) continue;
-            const int2 wv = s_fwin[sl];
-            const float v = s_tval[sl * TWN + tex * 3 + ch];
-            if (v == 0.f) continue;
-            const int x = wv.x + (tex & (TWIN - 1)), y = wv.y + tex / TWIN;
-            if (x < W && y < H) unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)y * W + x) * 4 + ch, v);
+    if (NR_ABLATE & 2) {
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int j = 0; j < 9; j++) asm volatile("" ::"v"(gF[k][j]));
+        return;
+    }
+    __syncthreads();  // the staged records reuse the image / gradient LDS
+
+    // ---- 3. stage this lane's two pixel records; group the wave's records by face --------------
+    float* rec = s_raw + wid * (128 * REC);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        float* r = rec + (k * 64 + lane) * REC;
+#pragma unroll
+        for (int j = 0; j < 9; j++) r[j] = gF[k][j];
+        r[9] = P[k].grgb[0];
+        r[10] = P[k].grgb[1];
+        r[11] = P[k].grgb[2];
+        r[12] = P[k].ay;
+        r[13] = P[k].by;
+        r[14] = P[k].ax;
+        r[15] = P[k].bx;
+        r[16] = __int_as_float(P[k].pos);
+    }
+    // output lane roles: 0..47 texel window (texel = lane / 3 as dx + 4 dy, channel lane % 3); 48..56 face floats
+    const int tt = lane / 3, tch = lane - 3 * tt;
+    const int tdx = tt & 3, tdy = tt >> 2;
+    const bool act0 = P[0].fi >= 0, act1 = P[1].fi >= 0;
+    unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
+    while (p0 | p1) {
+        const bool from0 = p0 != 0ull;
+        const int leader = from0 ? __builtin_ctzll(p0) : __builtin_ctzll(p1);
+        const int key = from0 ? __builtin_amdgcn_readlane(P[0].fi, leader) : __builtin_amdgcn_readlane(P[1].fi, leader);
+        const int wx = from0 ? __builtin_amdgcn_readlane(P[0].wx, leader) : __builtin_amdgcn_readlane(P[1].wx, leader);
+        const int wy = from0 ? __builtin_amdgcn_readlane(P[0].wy, leader) : __builtin_amdgcn_readlane(P[1].wy, leader);
+        const unsigned long long m0 = __ballot(act0 && P[0].fi == key) & p0;
+        const unsigned long long m1 = __ballot(act1 && P[1].fi == key) & p1;
+        p0 &= ~m0;
+        p1 &= ~m1;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            for (unsigned long long m = k ? m1 : m0; m; m &= m - 1) {
+                const float* r = rec + (k * 64 + __builtin_ctzll(m)) * REC;
+                if (lane < 48) {
+                    const int pos = __float_as_int(r[16]);
+                    const int cx = tdx - (pos & 0xff), cy = tdy - (pos >> 8);
+                    if (pos >= 0 && cx >= 0 && cx <= 1 && cy >= 0 && cy <= 1)
+                        acc += r[9 + tch] * ((cy ? r[13] : r[12]) * (cx ? r[15] : r[14]));
+                } else if (lane < 57) {
+                    acc += r[lane - 48];
+                }
+            }
+        }
+        // ---- 4. flush this face: 48 window lanes + 9 face-record lanes -------------------------
+        if (lane < 48) {
+            const int x = wx + tdx, y = wy + tdy;
+            if (want_tex && acc != 0.f && wx != INT_MIN && x < sh.tv.W && y < sh.tv.H)
+                unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)y * sh.tv.W + x) * 4 + tch, acc);
+        } else if (lane < 57) {
+            if (acc != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + (lane - 48), acc);
         }
     }
 }
@@ -1274,6 +1310,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.s = a->image_size;
     ba.HWp = HWp;
     ba.step = (float)(2. / S);
+    ba.inv_step = 1.f / ba.step;
+    ba.step_pow2 = (S & (S - 1)) == 0;  // step = 2/S is then a power of two: x / step == x * (S / 2)
     Shade sh = make_shade(a);
     hipLaunchKernelGGL(k_raster_bwd, dim3(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size), dim3(NT), 0, st, ba,
                        g, sh);

@@ -8,13 +8,15 @@
 //     (rasterize_cuda_kernel.cu:82-149; no FMA contraction, IEEE division, double pixel centres);
 //   * rgb / depth / silhouette values follow rasterize.py:80-153 operation for operation.
 //
-// Pipeline of one forward (3 launches) -- see DESIGN.md for the data layout and rooflines:
+// Pipeline of one forward (3 launches: setup, raster, shade) -- see DESIGN.md for the data layout and rooflines:
 //   k_face_setup     one block per (128 faces, item): gather the faces from vertices (rasterize.py:232),
 //                    per-face screen bbox + face-level rejects, texture-uv gather, and the coarse-bin
 //                    face bitmasks (64x64-pixel bins, bit f set when face f may touch the bin).
 //   k_raster_fwd     one block per 32x32-pixel coarse bin: stages the bin's candidate faces in face
-//                    order into LDS, each wave walks (ballot) the faces touching its pixels in order,
-//                    then shades rgb/sil/depth and writes fim + the flipped, 2x2-averaged output.
+//                    order into LDS, each wave walks (ballot) the faces touching its pixels in order;
+//                    writes the face-index map.
+//   k_shade          one thread per output pixel: weights, texture, silhouette, depth, merged,
+//                    flipped and 2x2-averaged into the [B, C, s, s] image.
 //   backward         k_raster_bwd: one block per 32x16 pixels + 1-pixel halo: recomputes the internal
 //                    image from fim, applies Differentiation.backward's stencil, and chains the
 //                    coordinate / depth / texture gradients to vertices and textures with atomics.
@@ -377,8 +379,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
 //      bits in order (scalar loop), running the reference's per-face test for its pixel -- every
 //      pixel therefore sees its candidate faces in ascending index order, as the reference's
 //      sequential loop does (.cu:82-149), and the per-pixel state stays in registers across rounds;
-//   4. shading of the 4 pixels (weights, texture, depth) and the flipped, 2x2-averaged output
-//      written through LDS in 64-byte rows.
+//   shading and the output image are computed by k_shade.
 //   LDS face record (7 x float4):
 //     0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
 //     4: z2 A=x1-x0 B=y1-y0 C=x2-x1 | 5: D=y2-y1 E=x0-x2 F=y0-y2 k0 | 6: k1 k2 - -
@@ -388,13 +389,7 @@ constexpr int FCAP = 128;                       // faces staged per round
 constexpr int FREC = 7;                         // float4 per staged face
 constexpr int NSUB = (COARSE * COARSE) / NT;    // pixels per thread (4)
 constexpr int FWD_LDS_FACES = FCAP * FREC * 16 + CAND * 4;
-constexpr int FWD_LDS_CHAN = MAXC * COARSE * COARSE * 4;
-constexpr int FWD_LDS = FWD_LDS_FACES > FWD_LDS_CHAN ? FWD_LDS_FACES : FWD_LDS_CHAN;
-
-struct FwdOut {
-    float* images;   // [B, C, s, s] (FUSED only)
-    int32_t* fim;    // [B, S, S]
-};
+constexpr int FWD_LDS = FWD_LDS_FACES;
 
 __device__ __forceinline__ void pixel_of(int t, int& lx, int& ly) {
     // 4 waves as a 2x2 grid of 16x4 pixel blocks of a 32x8 tile
@@ -451,15 +446,13 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
     e[6] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, 0.f, 0.f);
 }
 
-template <bool FUSED>
 __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, const int2* __restrict__ bbox,
                                                   const uint32_t* __restrict__ mask, int F, Geom g, float near,
-                                                  float far, float delta, Shade sh, int aa, FwdOut out) {
+                                                  float far, float delta, int32_t* __restrict__ fim) {
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[FWD_LDS];
     __shared__ int s_scan[4];
     float4(*s_face)[FREC] = reinterpret_cast<float4(*)[FREC]>(s_raw);
     int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
-    float* s_chan = reinterpret_cast<float*>(s_raw);  // after rasterisation: [C][NSUB][NT]
 
     const int b = blockIdx.y;
     const int S = g.S;
@@ -535,56 +528,56 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
         const int py = by0 + TH * k + ly;
-        if (px < S && py < S) out.fim[((long long)b * S + py) * S + px] = best[k];
+        if (px < S && py < S) fim[((long long)b * S + py) * S + px] = best[k];
     }
-    if (!FUSED) return;
+}
 
-    // shading: all four pixels' loads are independent
-    float v[NSUB][MAXC];
-#pragma unroll
-    for (int k = 0; k < NSUB; k++) {
-        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (best[k] >= 0) f = load_face(frb + (long long)best[k] * 9);
-        shade_pixel(sh, b, best[k], f, xp, yp[k], v[k]);
-    }
+// ------------------------------------------------------------------------------------------------
+// k_shade: the image channels from the face-index map, one thread per OUTPUT pixel (rasterize.py:
+// 237-328): weights (compute_weight_map), texture sample, silhouette and depth for the 1 or 2x2
+// internal pixels it covers, merged in rgb/sil/depth order, flipped, and 2x2-averaged with the
+// reference's summation order.  Kept out of the rasteriser so that kernel stays lean (registers,
+// occupancy); costs one extra read of the face-index map.
+__global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
+                                               int F, int S, Shade sh, int aa, float* __restrict__ images) {
+    const int s = aa ? S / 2 : S;
+    const int b = blockIdx.y;
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= s * s) return;
+    const int oi = o / s, oj = o - oi * s;
+    const float* frb = face_records + (long long)b * F * 9;
+    const int32_t* fb = fim + (long long)b * S * S;
+    float* ob = images + (long long)b * sh.C * s * s + o;
     if (!aa) {
-#pragma unroll
-        for (int k = 0; k < NSUB; k++) {
-            const int py = by0 + TH * k + ly;
-            if (px < S && py < S) {
-                // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
-#pragma unroll
-                for (int c = 0; c < MAXC; c++)
-                    if (c < sh.C)
-                        out.images[(((long long)b * sh.C + c) * S + (S - 1 - py)) * S + (S - 1 - px)] = v[k][c];
-            }
-        }
-        return;
-    }
-    __syncthreads();  // s_chan aliases the face stage
-#pragma unroll
-    for (int k = 0; k < NSUB; k++)
+        // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
+        const int y = S - 1 - oi, x = S - 1 - oj;
+        const int fi = fb[(long long)y * S + x];
+        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (fi >= 0) f = load_face(frb + (long long)fi * 9);
+        float v[MAXC];
+        shade_pixel(sh, b, fi, f, pix_center(x, S), pix_center(y, S), v);
 #pragma unroll
         for (int c = 0; c < MAXC; c++)
-            if (c < sh.C) s_chan[(c * NSUB + k) * NT + ly * TW + lx] = v[k][c];
-    __syncthreads();
-    // 2x2 average of the flipped image (rasterize.py:321-328): output pixel (ox, oy) of the bin reads
-    // internal rows iy, iy+1 and columns ix, ix+1 (iy, ix even): a=(iy+1,ix+1) b=(iy,ix+1) c=(iy+1,ix) d=(iy,ix)
-    {
-        const int ox = t % (COARSE / 2), oy = t / (COARSE / 2);
-        const int ix = bx0 + 2 * ox, iy = by0 + 2 * oy;
-        if (ix < S && iy < S) {
-            const int s = S / 2;
-            const int oi = (S - 2 - iy) / 2, oj = (S - 2 - ix) / 2;
-            const int k = (2 * oy) / TH;
-            const int l00 = ((2 * oy) % TH) * TW + 2 * ox;
-            for (int c = 0; c < sh.C; c++) {
-                const float* sc = s_chan + (c * NSUB + k) * NT;
-                const float a = sc[l00 + TW + 1], bq = sc[l00 + 1], cq = sc[l00 + TW], d = sc[l00];
-                out.images[(((long long)b * sh.C + c) * s + oi) * s + oj] = (((a + bq) + cq) + d) / 4.f;
-            }
-        }
+            if (c < sh.C) ob[(long long)c * s * s] = v[c];
+        return;
     }
+    // 2x2 average of the flipped image (rasterize.py:321-328): output (oi, oj) reads internal rows
+    // iy, iy+1 and columns ix, ix+1 with a=(iy+1,ix+1) b=(iy,ix+1) c=(iy+1,ix) d=(iy,ix)
+    const int iy = S - 2 - 2 * oi, ix = S - 2 - 2 * oj;
+    const int2 f0 = *reinterpret_cast<const int2*>(fb + (long long)iy * S + ix);        // d, b
+    const int2 f1 = *reinterpret_cast<const int2*>(fb + (long long)(iy + 1) * S + ix);  // c, a
+    const int fis[4] = {f1.y, f0.y, f1.x, f0.x};
+    const int ys[4] = {iy + 1, iy, iy + 1, iy}, xs[4] = {ix + 1, ix + 1, ix, ix};
+    float v[4][MAXC];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (fis[q] >= 0) f = load_face(frb + (long long)fis[q] * 9);
+        shade_pixel(sh, b, fis[q], f, pix_center(xs[q], S), pix_center(ys[q], S), v[q]);
+    }
+#pragma unroll
+    for (int c = 0; c < MAXC; c++)
+        if (c < sh.C) ob[(long long)c * s * s] = (((v[0][c] + v[1][c]) + v[2][c]) + v[3][c]) / 4.f;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1196,20 +1189,14 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         int e = check_launch("k_face_setup");
         if (e) return e;
     }
-    FwdOut out;
-    out.fim = fim;
-    out.images = images;
-    dim3 grid(g.nbins, B);
-    if (ra) {
-        Shade sh = make_shade(ra);
-        hipLaunchKernelGGL(k_raster_fwd<true>, grid, dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far, delta,
-                           sh, ra->anti_aliasing, out);
-    } else {
-        Shade sh = {};
-        hipLaunchKernelGGL(k_raster_fwd<false>, grid, dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far, delta,
-                           sh, 0, out);
-    }
-    return check_launch("k_raster_fwd");
+    hipLaunchKernelGGL(k_raster_fwd, dim3(g.nbins, B), dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far,
+                       delta, fim);
+    int e = check_launch("k_raster_fwd");
+    if (e || !ra) return e;
+    const int s = ra->anti_aliasing ? S / 2 : S;
+    hipLaunchKernelGGL(k_shade, dim3((unsigned)(((long long)s * s + 255) / 256), B), dim3(256), 0, st, face_records, fim,
+                       F, S, make_shade(ra), ra->anti_aliasing, images);
+    return check_launch("k_shade");
 }
 
 int nr_face_index_map_forward_safe(const float* faces, int32_t* face_index, int batch_size, int num_faces,

@@ -401,6 +401,10 @@ __device__ __forceinline__ void pixel_of(int t, int& lx, int& ly) {
 // the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel
 __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, float near, float far, float delta,
                                           float& depth_min, int& best) {
+#if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 1
+    best += (int)e[0].x;  // timing build: no per-pixel test
+    return;
+#endif
     const float4 q0 = e[0];
     // .cu:94-97 (min/max form, exact for non-NaN faces)
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
@@ -415,6 +419,10 @@ __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, f
     const float4 q1 = e[1];
     // .cu:124-126
     if (depth_min < q1.z) return;
+#if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 2
+    best = __float_as_int(q1.w);  // timing build: no division block
+    return;
+#endif
     const float4 q6 = e[6];
     const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
     // .cu:130-139
@@ -705,12 +713,13 @@ constexpr int BH = 16;                        // block height
 constexpr int HW_ = TW + 2, HH_ = BH + 2, HN = HW_ * HH_;
 constexpr int NHALO = 2 * HW_ + 2 * BH;       // 100 halo pixels
 constexpr int TWIN = 4;                       // texel window edge per face
-constexpr int REC = 17;                       // staged record: gF[9] G_rgb[3] ay by ax bx pos
+constexpr int REC = 20;                       // staged record: ay by ax bx | pos G_rgb[3] | gF[9] | pad
 constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
 constexpr int BWD_LDS_REC = 4 * 128 * REC * 4;
 constexpr int BWD_LDS = BWD_LDS_IG > BWD_LDS_REC ? BWD_LDS_IG : BWD_LDS_REC;
 // experiment switch for timing builds (never set in the shipped library):
-//   2 = no gradient accumulation (steps 3 and 4)
+//   2 = no gradient accumulation (steps 3 and 4), 4 = no global atomics (step 4),
+//   8 = no per-face gather (step 3's member loop)
 #ifndef NR_ABLATE
 #define NR_ABLATE 0
 #endif
@@ -1025,20 +1034,18 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         float* r = rec + (k * 64 + lane) * REC;
+        reinterpret_cast<float4*>(r)[0] = make_float4(P[k].ay, P[k].by, P[k].ax, P[k].bx);
+        reinterpret_cast<float4*>(r)[1] = make_float4(__int_as_float(P[k].pos), P[k].grgb[0], P[k].grgb[1], P[k].grgb[2]);
 #pragma unroll
-        for (int j = 0; j < 9; j++) r[j] = gF[k][j];
-        r[9] = P[k].grgb[0];
-        r[10] = P[k].grgb[1];
-        r[11] = P[k].grgb[2];
-        r[12] = P[k].ay;
-        r[13] = P[k].by;
-        r[14] = P[k].ax;
-        r[15] = P[k].bx;
-        r[16] = __int_as_float(P[k].pos);
+        for (int j = 0; j < 9; j++) r[8 + j] = gF[k][j];
     }
-    // output lane roles: 0..47 texel window (texel = lane / 3 as dx + 4 dy, channel lane % 3); 48..56 face floats
-    const int tt = lane / 3, tch = lane - 3 * tt;
+    // output lane roles: texel t = lane & 15 of the face's 4x4 window (dx = t & 3, dy = t >> 2), member
+    // chunk c = lane >> 4: lane (t, c) sums the 3 channel contributions to texel t (and, for t < 9,
+    // face-gradient float t) over the face's records whose pixel lies in row c of the wave's 16x4
+    // sub-blocks; the 4 chunks are then added across lanes.
+    const int tt = lane & 15, chunk = lane >> 4;
     const int tdx = tt & 3, tdy = tt >> 2;
+    const int fsel = 8 + (tt < 9 ? tt : 0);
     const bool act0 = P[0].fi >= 0, act1 = P[1].fi >= 0;
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
     while (p0 | p1) {
@@ -1051,28 +1058,47 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         const unsigned long long m1 = __ballot(act1 && P[1].fi == key) & p1;
         p0 &= ~m0;
         p1 &= ~m1;
-        float acc = 0.f;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f;
+        if (!(NR_ABLATE & 8)) {
+            // this lane's members: row `chunk` of each 16x4 sub-block (lanes 16 chunk .. 16 chunk + 15)
+            unsigned mine[2] = {(unsigned)(m0 >> (16 * chunk)) & 0xffffu, (unsigned)(m1 >> (16 * chunk)) & 0xffffu};
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            for (unsigned long long m = k ? m1 : m0; m; m &= m - 1) {
-                const float* r = rec + (k * 64 + __builtin_ctzll(m)) * REC;
-                if (lane < 48) {
-                    const int pos = __float_as_int(r[16]);
+            for (int k = 0; k < 2; k++) {
+                for (unsigned m = mine[k]; m; m &= m - 1) {
+                    const float* r = rec + (k * 64 + 16 * chunk + __builtin_ctz(m)) * REC;
+                    const int pos = __float_as_int(r[4]);
                     const int cx = tdx - (pos & 0xff), cy = tdy - (pos >> 8);
-                    if (pos >= 0 && cx >= 0 && cx <= 1 && cy >= 0 && cy <= 1)
-                        acc += r[9 + tch] * ((cy ? r[13] : r[12]) * (cx ? r[15] : r[14]));
-                } else if (lane < 57) {
-                    acc += r[lane - 48];
+                    const bool hit = pos >= 0 && cx >= 0 && cx <= 1 && cy >= 0 && cy <= 1;
+                    const float wt = r[cy & 1] * r[2 + (cx & 1)];
+                    const float g0 = r[5], g1 = r[6], g2 = r[7];
+                    if (hit) {
+                        a0 += g0 * wt;
+                        a1 += g1 * wt;
+                        a2 += g2 * wt;
+                    }
+                    af += r[fsel];
                 }
             }
         }
-        // ---- 4. flush this face: 48 window lanes + 9 face-record lanes -------------------------
-        if (lane < 48) {
+        // add the 4 member chunks (lanes t, t+16, t+32, t+48)
+        a0 += __shfl_xor(a0, 16, 64);
+        a1 += __shfl_xor(a1, 16, 64);
+        a2 += __shfl_xor(a2, 16, 64);
+        af += __shfl_xor(af, 16, 64);
+        a0 += __shfl_xor(a0, 32, 64);
+        a1 += __shfl_xor(a1, 32, 64);
+        a2 += __shfl_xor(a2, 32, 64);
+        af += __shfl_xor(af, 32, 64);
+        // ---- 4. flush this face: lane (t, c) writes channel c of texel t (c < 3) or face float t (c == 3)
+        const float v = chunk == 0 ? a0 : (chunk == 1 ? a1 : (chunk == 2 ? a2 : af));
+        if (NR_ABLATE & 4) {
+            asm volatile("" ::"v"(v));
+        } else if (chunk < 3) {
             const int x = wx + tdx, y = wy + tdy;
-            if (want_tex && acc != 0.f && wx != INT_MIN && x < sh.tv.W && y < sh.tv.H)
-                unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)y * sh.tv.W + x) * 4 + tch, acc);
-        } else if (lane < 57) {
-            if (acc != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + (lane - 48), acc);
+            if (want_tex && v != 0.f && wx != INT_MIN && x < sh.tv.W && y < sh.tv.H)
+                unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)y * sh.tv.W + x) * 4 + chunk, v);
+        } else if (tt < 9) {
+            if (v != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + tt, v);
         }
     }
 }

@@ -1,9 +1,14 @@
-# usage: bash tools/pmc.sh <tag>: PMC counter passes (one rocprofv3 run per pass) over a short bench
+# usage: [NR_ABLATE=n] bash tools/pmc.sh <tag>: PMC counter passes (one rocprofv3 run per pass) over a short bench
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-pmc}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
+if [ -n "$NR_ABLATE" ]; then
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math \
+    -fvisibility=hidden -Iinclude -DNR_ABLATE=$NR_ABLATE neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip -o /tmp/libnr_pmc.so || exit 1
+  export NR_LIB_PATH=/tmp/libnr_pmc.so
+fi
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1
 i=0
 while read -r PASS; do
@@ -15,7 +20,5 @@ while read -r PASS; do
 done <<'PASSES'
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES
 SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS
-FETCH_SIZE
-WRITE_SIZE
-GRBM_GUI_ACTIVE SQ_INSTS_FLAT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM
+GRBM_GUI_ACTIVE SQ_INSTS_FLAT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH
 PASSES

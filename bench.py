@@ -95,34 +95,65 @@ def step(w):
 
 
 def kernel_bytes(w, args):
-    """Algorithmic (compulsory) bytes per launch of each kernel, SURVEY.md section 8d / DESIGN.md."""
+    """Algorithmic (compulsory) HBM bytes per launch of each kernel (DESIGN.md "Kernels"): what the
+    kernel must read and write at minimum, with stride-0 batch-expanded tensors counted once."""
     B, s, C, V, F = args.batch, args.image_size, w["C"], w["V"], w["F"]
     S = 2 * s
-    T = 0 if w["tex_shape"] is None else 3 * w["tex_shape"][1] * w["tex_shape"][2] * 4
-    fwd = 4 * S * S * B + 4 * C * s * s * B + 36 * F * B + T
-    bwd = 4 * S * S * B + 4 * C * s * s * B + 36 * F * B + 12 * V * B + 2 * T
-    setup = 12 * V * B + 12 * F + 36 * F * B + 8 * F * B
+    rgb = w["tex_shape"] is not None
+    T = 3 * w["tex_shape"][1] * w["tex_shape"][2] * 4 if rgb else 0
+    fim, img, frec = 4 * S * S * B, 4 * C * s * s * B, 36 * F * B
+    k = {
+        "k_face_setup": 12 * V * B + 12 * F + frec + (24 * F + 12 * F if rgb else 0),
+        "k_raster_fwd": frec + fim,
+        "k_shade": fim + frec + (24 * F + T if rgb else 0) + img,
+        "k_raster_bwd": fim + img + frec + (24 * F + T + T if rgb else 0) + frec,
+        "k_vertex_grad": frec + 4 * (V + 1) + 12 * F + 12 * V * B,
+        "k_tex_out": 2 * T,
+    }
     total = B * (8 * S * S + 8 * C * s * s + 36 * V) + 24 * F + (2 * T if T else 0)
-    return dict(fwd=fwd, bwd=bwd, setup=setup, total=total)
+    return k, total
+
+
+KERNELS = ["k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
 
 
 def time_kernels(w, n=10):
-    """HIP-event timing of the library's forward and backward calls on the launch stream."""
-    from neural_renderer_v2_pytorch_amd.rasterize import rasterize_core
-    stream = torch.cuda.current_stream()
-    fwd_ms, bwd_ms = [], []
-    for _ in range(n):
-        w["proj"].grad = None
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-        e0.record(stream)
-        images = rasterize_core(w["proj"], w["faces"], w["params"], w["hp"])
-        e1.record(stream)
-        images.backward(w["g"])
-        e2.record(stream)
-        torch.cuda.synchronize()
-        fwd_ms.append(e0.elapsed_time(e1))
-        bwd_ms.append(e1.elapsed_time(e2))
-    return float(np.median(fwd_ms)), float(np.median(bwd_ms))
+    """Per-kernel durations from HIP events the library records on its launch stream around each
+    launch (nr_profile_enable / nr_profile_read), averaged over n fwd+bwd calls."""
+    import ctypes
+    from neural_renderer_v2_pytorch_amd import _lib
+    L = _lib.lib()
+    _lib.check(L.nr_profile_enable(1), "nr_profile_enable")
+    acc = {k: [] for k in KERNELS}
+    try:
+        for _ in range(n):
+            step(w)
+            torch.cuda.synchronize()
+            for k in KERNELS:
+                ms = ctypes.c_float()
+                if L.nr_profile_read(k.encode(), ctypes.byref(ms)) == 0:
+                    acc[k].append(ms.value)
+    finally:
+        L.nr_profile_enable(0)
+    return {k: float(np.mean(v)) for k, v in acc.items() if v}
+
+
+def copy_ceiling_gbs(dev, nbytes=1 << 30, reps=10):
+    """Achievable HBM stream rate on this box: a 1 GiB -> 1 GiB elementwise stream (16 B per lane
+    loads and stores), read + write bytes.  tools/pmc_traffic.py also uses these launches, of known
+    byte count, to calibrate the FETCH_SIZE / WRITE_SIZE counters."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    torch.mul(src, 2.0, out=dst)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.mul(src, 2.0, out=dst)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    return gbs
 
 
 def cpu_baseline(args, budget_s):
@@ -198,11 +229,12 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - t1) * 1e3
 
-    fwd_ms, bwd_ms = time_kernels(w)
-    kb = kernel_bytes(w, args)
-    dominant, dom_ms = ("k_raster_bwd", bwd_ms) if bwd_ms >= fwd_ms else ("k_face_setup+k_raster_fwd", fwd_ms)
-    dom_bytes = kb["bwd"] if dominant == "k_raster_bwd" else kb["fwd"] + kb["setup"]
+    kms = time_kernels(w)
+    kb, total_bytes = kernel_bytes(w, args)
+    dominant = max(kms, key=kms.get)
+    dom_ms, dom_bytes = kms[dominant], kb[dominant]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    ceiling = copy_ceiling_gbs(dev)
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -234,9 +266,10 @@ def main():
                    "channels": w["C"], "parallelism": "batch-sharded dp%d" % world},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5)},
-        "kernels_ms": {"fwd": round(fwd_ms, 5), "bwd": round(bwd_ms, 5)},
-        "step_roofline_frac": round(kb["total"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                     "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5),
+                     "copy_ceiling_gbs": round(ceiling, 1)},
+        "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
+        "step_roofline_frac": round(total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
     }
     if gather_ms is not None:
         res["gather_ms"] = round(gather_ms, 4)

@@ -135,6 +135,14 @@ NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int tex
 NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
                                  float* grad_textures, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Measurement hook (bench.py's roofline leg; no reference counterpart).  With profiling on, the
+ * library brackets each launch of its kernels with a pair of HIP events recorded on the launch
+ * stream; nr_profile_read gives the duration in ms of the most recent launch of `kernel`
+ * ("k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out") once
+ * the stream has been synchronised.  Process-wide state, meant for a single measuring thread. */
+NR_API int nr_profile_enable(int on);
+NR_API int nr_profile_read(const char* kernel, float* ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,7 +22,7 @@ EXPORTS = [
     "nr_last_error", "nr_version", "nr_workspace_bytes", "nr_face_index_map_forward_safe",
     "nr_compute_weight_map", "nr_mask_foreground_forward", "nr_mask_foreground_backward",
     "nr_differentiation_backward", "nr_num_channels", "nr_rasterize_forward", "nr_rasterize_backward",
-    "nr_backward_workspace_bytes",
+    "nr_backward_workspace_bytes", "nr_profile_enable", "nr_profile_read",
 ]
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
@@ -73,6 +73,8 @@ def lib():
                                         c_size_t, c_void_p]
     L.nr_backward_workspace_bytes.restype = c_size_t
     L.nr_backward_workspace_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int]
+    L.nr_profile_enable.argtypes = [c_int]
+    L.nr_profile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(c_float)]
     for name in EXPORTS:
         if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels", "nr_backward_workspace_bytes"):
             getattr(L, name).restype = c_int

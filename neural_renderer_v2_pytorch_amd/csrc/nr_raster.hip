@@ -11,7 +11,7 @@
 // Pipeline of one forward (3 launches: setup, raster, shade) -- see DESIGN.md for the data layout and rooflines:
 //   k_face_setup     one block per (128 faces, item): gather the faces from vertices (rasterize.py:232),
 //                    per-face screen bbox + face-level rejects, texture-uv gather, and the coarse-bin
-//                    face bitmasks (64x64-pixel bins, bit f set when face f may touch the bin).
+//                    face bitmasks (32x32-pixel bins, bit f set when face f may touch the bin).
 //   k_raster_fwd     one block per 32x32-pixel coarse bin: stages the bin's candidate faces in face
 //                    order into LDS, each wave walks (ballot) the faces touching its pixels in order;
 //                    writes the face-index map.
@@ -27,6 +27,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <string>
 
@@ -40,7 +41,6 @@ constexpr int TW = 32;             // tile width  (internal pixels)
 constexpr int TH = 8;              // tile height
 constexpr int NT = TW * TH;        // threads per raster block, one pixel each
 constexpr int COARSE = 32;         // coarse bin edge (pixels) = forward block region; = TW, multiple of TH
-constexpr int CAP = 256;           // faces staged in LDS per round
 constexpr int SETUP_FACES = 128;   // faces per setup block (4 bitmask words)
 constexpr int MAXC = 5;            // max output channels
 
@@ -64,6 +64,28 @@ int check_launch(const char* what) {
     }
     return NR_OK;
 }
+
+// ---- measurement hook (nr_profile_enable / nr_profile_read) ----
+enum { P_SETUP, P_RASTER, P_SHADE, P_BWD, P_VGRAD, P_TEXOUT, P_N };
+const char* const kProfNames[P_N] = {"k_face_setup", "k_raster_fwd", "k_shade",
+                                     "k_raster_bwd", "k_vertex_grad", "k_tex_out"};
+bool g_prof = false;
+hipEvent_t g_prof_ev[P_N][2];
+bool g_prof_rec[P_N];
+
+struct ProfScope {  // records the start/end events of one launch when profiling is on
+    int k;
+    hipStream_t st;
+    ProfScope(int k_, hipStream_t s) : k(k_), st(s) {
+        if (g_prof) (void)hipEventRecord(g_prof_ev[k][0], st);
+    }
+    ~ProfScope() {
+        if (g_prof) {
+            (void)hipEventRecord(g_prof_ev[k][1], st);
+            g_prof_rec[k] = true;
+        }
+    }
+};
 
 struct Geom {
     int S, nbx, nby, nbins, nwords, tiles_x, tiles_y;
@@ -1203,6 +1225,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         dim3 grid((F + SETUP_FACES - 1) / SETUP_FACES, B);
         const bool rgb = ra && (ra->draw_flags & NR_DRAW_RGB);
         const int uv_items = rgb ? (ra->vt_batch_stride ? B : 1) : 0;
+        ProfScope _p(P_SETUP, st);
         if (vertices)
             hipLaunchKernelGGL(k_face_setup<true>, grid, dim3(256), 0, st, vertices, faces_idx, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
@@ -1215,13 +1238,19 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         int e = check_launch("k_face_setup");
         if (e) return e;
     }
-    hipLaunchKernelGGL(k_raster_fwd, dim3(g.nbins, B), dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far,
-                       delta, fim);
+    {
+        ProfScope _p(P_RASTER, st);
+        hipLaunchKernelGGL(k_raster_fwd, dim3(g.nbins, B), dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far,
+                           delta, fim);
+    }
     int e = check_launch("k_raster_fwd");
     if (e || !ra) return e;
     const int s = ra->anti_aliasing ? S / 2 : S;
-    hipLaunchKernelGGL(k_shade, dim3((unsigned)(((long long)s * s + 255) / 256), B), dim3(256), 0, st, face_records, fim,
-                       F, S, make_shade(ra), ra->anti_aliasing, images);
+    {
+        ProfScope _p(P_SHADE, st);
+        hipLaunchKernelGGL(k_shade, dim3((unsigned)(((long long)s * s + 255) / 256), B), dim3(256), 0, st, face_records, fim,
+                           F, S, make_shade(ra), ra->anti_aliasing, images);
+    }
     return check_launch("k_shade");
 }
 
@@ -1326,23 +1355,59 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.inv_step = 1.f / ba.step;
     ba.step_pow2 = (S & (S - 1)) == 0;  // step = 2/S is then a power of two: x / step == x * (S / 2)
     Shade sh = make_shade(a);
-    hipLaunchKernelGGL(k_raster_bwd, dim3(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size), dim3(NT), 0, st, ba,
-                       g, sh);
+    {
+        ProfScope _p(P_BWD, st);
+        hipLaunchKernelGGL(k_raster_bwd, dim3(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size), dim3(NT), 0, st, ba,
+                           g, sh);
+    }
     e = check_launch("k_raster_bwd");
     if (e) return e;
     const long long nv = (long long)a->batch_size * a->num_vertices;
     if (nv > 0) {
-        hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gF, a->vertex_offsets,
-                           a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv);
+        {
+            ProfScope _p(P_VGRAD, st);
+            hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gF, a->vertex_offsets,
+                               a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv);
+        }
         e = check_launch("k_vertex_grad");
         if (e) return e;
     }
     if (rgb) {
         const long long nt = (long long)tex_items * HW;
-        hipLaunchKernelGGL(k_tex_out, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, g4, grad_textures, HW, HWp, nt);
+        {
+            ProfScope _p(P_TEXOUT, st);
+            hipLaunchKernelGGL(k_tex_out, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, g4, grad_textures, HW, HWp, nt);
+        }
         e = check_launch("k_tex_out");
     }
     return e;
+}
+
+int nr_profile_enable(int on) {
+    if (on && !g_prof) {
+        for (int k = 0; k < P_N; k++)
+            for (int j = 0; j < 2; j++)
+                if (hipEventCreate(&g_prof_ev[k][j]) != hipSuccess) return fail(NR_ERR_LAUNCH, "hipEventCreate failed");
+    } else if (!on && g_prof) {
+        for (int k = 0; k < P_N; k++)
+            for (int j = 0; j < 2; j++) (void)hipEventDestroy(g_prof_ev[k][j]);
+    }
+    if (!on || !g_prof)
+        for (int k = 0; k < P_N; k++) g_prof_rec[k] = false;
+    g_prof = on != 0;
+    return NR_OK;
+}
+
+int nr_profile_read(const char* kernel, float* ms) {
+    if (!kernel || !ms) return fail(NR_ERR_ARGS, "null argument");
+    for (int k = 0; k < P_N; k++) {
+        if (strcmp(kernel, kProfNames[k]) != 0) continue;
+        if (!g_prof || !g_prof_rec[k]) return fail(NR_ERR_ARGS, "%s: no profiled launch recorded", kernel);
+        if (hipEventElapsedTime(ms, g_prof_ev[k][0], g_prof_ev[k][1]) != hipSuccess)
+            return fail(NR_ERR_LAUNCH, "%s: hipEventElapsedTime failed", kernel);
+        return NR_OK;
+    }
+    return fail(NR_ERR_ARGS, "unknown kernel name %s", kernel);
 }
 
 }  // extern "C"

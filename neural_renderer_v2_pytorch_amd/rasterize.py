@@ -232,12 +232,17 @@ class Rasterize(torch.autograd.Function):
         ctx.save_for_backward(vertices, textures, vertices_textures, faces, faces_textures, face_records, face_uv,
                               fim)
         ctx.mark_non_differentiable(fim)
+        # no zero-filled gradient for the int32 face-index output (a 67 MB fill per backward at the
+        # headline size otherwise)
+        ctx.set_materialize_grads(False)
         return images, fim
 
     @staticmethod
     def backward(ctx, grad_images, _grad_fim):
         cfg = ctx.cfg
         vertices, textures, vt, faces, ft, face_records, face_uv, fim = ctx.saved_tensors
+        if grad_images is None:
+            return None, None, None, None, None, None
         grad_images = grad_images.contiguous()
         L = _lib.lib()
         dev = vertices.device

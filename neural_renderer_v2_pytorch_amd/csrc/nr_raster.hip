@@ -281,6 +281,63 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
 }
 
 // ------------------------------------------------------------------------------------------------
+// XCD-aware block -> tile map.  Workgroups go round-robin to the 8 XCDs (linear id % 8) and each XCD
+// has its own L2, so with the identity map horizontally adjacent tiles never share a cache, and the
+// halo columns, upstream-gradient lines and face records they have in common are fetched once per
+// XCD.  Two remaps (measured on the headline workload):
+//   mode 1 (groups): runs of SW x SH neighbouring tiles go to one XCD back to back; groups
+//          interleave over the XCDs.  Full tile rows (SW = nx, SH = 1) are the balanced case.
+//   mode 2 (bands):  XCD x takes a band of ny / 8 whole tile rows of each item, the band rotating
+//          with the item so every XCD sees every band over 8 items (balanced over the batch).
+// Both fall back to the identity when the grid does not divide evenly (the linear id of item b
+// starts at b * nx * ny, a multiple of 8 whenever the remap applies).
+#ifndef NR_SWZ_MODE
+#define NR_SWZ_MODE 2
+#endif
+#ifndef NR_SWZ_W
+#define NR_SWZ_W 0  // 0: the full tile row
+#endif
+#ifndef NR_SWZ_H
+#define NR_SWZ_H 1
+#endif
+#ifndef NR_FSWZ_MODE
+#define NR_FSWZ_MODE 2
+#endif
+#ifndef NR_FSWZ_W
+#define NR_FSWZ_W 0
+#endif
+#ifndef NR_SSWZ_MODE
+#define NR_SSWZ_MODE 0
+#endif
+#ifndef NR_FSWZ_H
+#define NR_FSWZ_H 1
+#endif
+template <int MODE, int SW_, int SH>
+__device__ __forceinline__ void xcd_tile(int L, int b, int nx, int ny, int& tx, int& ty) {
+    tx = L % nx;
+    ty = L / nx;
+    if (MODE == 1) {
+        const int SW = SW_ > 0 ? SW_ : nx;
+        const int per = SW * SH;
+        const int ngx = nx / SW;
+        if (per > 1 && nx % SW == 0 && ny % SH == 0 && (ngx * (ny / SH)) % 8 == 0) {
+            const int j = L >> 3, xcd = L & 7;
+            const int grp = (j / per) * 8 + xcd;
+            const int q = j % per;
+            tx = (grp % ngx) * SW + q % SW;
+            ty = (grp / ngx) * SH + q / SW;
+        }
+    } else if (MODE == 2) {
+        if (ny % 8 == 0) {
+            const int j = L >> 3, xcd = L & 7;
+            const int band = (xcd + b) & 7;
+            tx = j % nx;
+            ty = band * (ny >> 3) + j / nx;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // block-wide exclusive scan of one int per thread (NT threads, 4 waves)
 __device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -486,8 +543,11 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
 
     const int b = blockIdx.y;
     const int S = g.S;
-    const int bx0 = (blockIdx.x % g.nbx) * COARSE;
-    const int by0 = (blockIdx.x / g.nbx) * COARSE;
+    int bin_x, bin_y;
+    xcd_tile<NR_FSWZ_MODE, NR_FSWZ_W, NR_FSWZ_H>(blockIdx.x, b, g.nbx, g.nby, bin_x, bin_y);
+    const int bin = bin_y * g.nbx + bin_x;
+    const int bx0 = bin_x * COARSE;
+    const int by0 = bin_y * COARSE;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     int lx, ly;
@@ -507,7 +567,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
     const int wx0 = bx0 + (wid & 1) * 16, wx1 = wx0 + 15;
     const int wy0 = by0 + (wid >> 1) * 4;
 
-    const uint32_t* words = mask + ((long long)b * g.nbins + blockIdx.x) * g.nwords;
+    const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
     const int2* bbb = bbox + (long long)b * F;
     const float* frb = face_records + (long long)b * F * 9;
 
@@ -572,7 +632,9 @@ __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_re
                                                int F, int S, Shade sh, int aa, float* __restrict__ images) {
     const int s = aa ? S / 2 : S;
     const int b = blockIdx.y;
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    int blk = blockIdx.x, unused;
+    xcd_tile<NR_SSWZ_MODE, 1, 1>(blockIdx.x, b, 1, gridDim.x, unused, blk);
+    const int o = blk * blockDim.x + threadIdx.x;
     if (o >= s * s) return;
     const int oi = o / s, oj = o - oi * s;
     const float* frb = face_records + (long long)b * F * 9;
@@ -813,9 +875,10 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
     const int C = sh.C;
     const bool rgb = (sh.draw & NR_DRAW_RGB) != 0;
     const bool want_tex = rgb && a.grad_tex4 != nullptr;
-    const int bxs = (S + TW - 1) / TW;
-    const int tx0 = (blockIdx.x % bxs) * TW;
-    const int ty0 = (blockIdx.x / bxs) * BH;
+    int tile_x, tile_y;
+    xcd_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(blockIdx.x, b, (S + TW - 1) / TW, (S + BH - 1) / BH, tile_x, tile_y);
+    const int tx0 = tile_x * TW;
+    const int ty0 = tile_y * BH;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     const int bt = sh.tv.sb ? b : 0;

@@ -126,3 +126,17 @@ def test_product_never_imports_oracle():
                 src = open(os.path.join(dirpath, fn)).read()
                 assert not re.search(r"^\s*(import|from)\s+oracle", src, re.M), fn
                 assert "libnr_oracle" not in src, fn
+
+
+def test_reference_binding_module_checks_inputs():
+    """rasterize_cuda mirrors the reference's CHECK_INPUT (cuda/rasterize_cuda.cpp:5-7): a CPU or
+    non-contiguous tensor raises RuntimeError before any launch; the dead unsafe kernel is refused."""
+    from neural_renderer_v2_pytorch_amd import rasterize_cuda as rc
+    faces = torch.zeros((1, 2, 3, 3))
+    fi = torch.zeros(16, dtype=torch.int32) - 1
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        rc.face_index_map_forward_safe(faces, fi, 2, 4, 0.1, 100., 1, 1e-8, 1e-4)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        rc.compute_weight_map_c(faces, fi, torch.zeros(16, 3), 2, 4)
+    with pytest.raises(NotImplementedError):
+        rc.face_index_map_forward_unsafe(faces, fi, None, None, 2, 4, 0.1, 100., 1, 1e-8)

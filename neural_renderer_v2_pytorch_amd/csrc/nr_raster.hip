@@ -148,6 +148,30 @@ __device__ __forceinline__ Face load_face(const float* __restrict__ fr) {
 __device__ __forceinline__ float t_max(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a > b ? a : b); }
 __device__ __forceinline__ float t_min(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a < b ? a : b); }
 
+// ---- exact division without the scaling / fix-up steps --------------------------------------
+// gfx950 lowers an IEEE binary32 a / b to
+//   v_div_scale(b), v_rcp, v_div_scale(a), r = fma(fma(-b, rcp, 1), rcp, rcp), q = a * r,
+//   q = fma(fma(-b, q, a), r, q), v_div_fmas(fma(-b, q, a), r, q), v_div_fixup.
+// v_div_scale leaves its operand unchanged and clears VCC, and v_div_fixup returns its input, unless
+// an operand is zero / inf / NaN / denormal, the quotient or 1/b is denormal, the numerator is below
+// 2^-103, or the exponents differ by 96 or more.  Outside those cases the sequence is exactly
+// rcp_nr + div_nr below, so div_nr is bit-identical to a / b there, and a reciprocal shared by
+// several divisions by the same b is computed once.  Callers guard the operand ranges (DESIGN.md
+// "Numerics"); a zero numerator may come out as +0 where a / b gives -0, which no caller observes.
+__device__ __forceinline__ float rcp_nr(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, r, 1.f), r, r);
+}
+__device__ __forceinline__ float div_nr(float a, float b, float r) {
+    float q = a * r;
+    q = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+// |x| in [2^-e, 2^e]
+__device__ __forceinline__ bool in_range(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }
+// coordinate / depth magnitudes for which the face-level guard below holds: 0 or [2^-20, 2^20]
+__device__ __forceinline__ bool coord_ok(float x) { return x == 0.f || in_range(x, 0x1p-20f, 0x1p20f); }
+
 // compute_weight_map_cuda_kernel (.cu:286-306)
 __device__ __forceinline__ void face_weights(float xp, float yp, const Face& f, float w[3]) {
     w[0] = yp * (f.x2 - f.x1) + xp * (f.y1 - f.y2) + (f.x1 * f.y2 - f.x2 * f.y1);
@@ -465,16 +489,33 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
 //   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
 constexpr int CAND = 512;                       // candidate ids expanded per round
 constexpr int FCAP = 128;                       // faces staged per round
-constexpr int FREC = 7;                         // float4 per staged face
+constexpr int FREC = 8;                         // float4 per staged face
 constexpr int NSUB = (COARSE * COARSE) / NT;    // pixels per thread (4)
-constexpr int FWD_LDS_FACES = FCAP * FREC * 16 + CAND * 4;
+constexpr int FWD_LDS_FACES = FCAP * FREC * 16 + FCAP * 16 + CAND * 4;
 constexpr int FWD_LDS = FWD_LDS_FACES;
 
-__device__ __forceinline__ void pixel_of(int t, int& lx, int& ly) {
-    // 4 waves as a 2x2 grid of 16x4 pixel blocks of a 32x8 tile
+#ifndef NR_FWD_SHAPE
+#define NR_FWD_SHAPE 1
+#endif
+// pixel (lx, ly) of thread t in sub-tile k of the 32x32 bin, and the origin (ox, oy) of its wave's
+// pixel block in that sub-tile.
+//   shape 0: each sub-tile is a 32x8 strip, the 4 waves own 16x4 blocks of it;
+//   shape 1: each wave owns a 16x16 quadrant, walked as four 8x8 blocks (less block perimeter per
+//            pixel, so fewer faces overlap a wave's block).
+constexpr int WBW = NR_FWD_SHAPE ? 8 : 16, WBH = NR_FWD_SHAPE ? 8 : 4;  // wave block
+__device__ __forceinline__ void pixel_of(int t, int k, int& lx, int& ly, int& ox, int& oy) {
     const int w = t >> 6, l = t & 63;
-    lx = (w & 1) * 16 + (l & 15);
-    ly = (w >> 1) * 4 + (l >> 4);
+    if (NR_FWD_SHAPE) {
+        ox = (w & 1) * 16 + (k & 1) * 8;
+        oy = (w >> 1) * 16 + (k >> 1) * 8;
+        lx = ox + (l & 7);
+        ly = oy + (l >> 3);
+    } else {
+        ox = (w & 1) * 16;
+        oy = (w >> 1) * 4 + TH * k;
+        lx = ox + (l & 15);
+        ly = oy + (l >> 4);
+    }
 }
 
 // the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel
@@ -509,10 +550,29 @@ __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, f
     float w1 = (yp * q5.y - xp * q5.z) + q6.x;
     float w2 = (yp * q4.y - xp * q4.z) + q6.y;
     const float ws = w0 + w1 + w2;
-    w0 /= ws;
-    w1 /= ws;
-    w2 /= ws;
-    const float zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
+    float zp;
+    const float4 q7 = e[7];
+    if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
+        // face coordinates and depths within [2^-20, 2^20] (or 0) bound every operand below inside
+        // div_nr's exact range (DESIGN.md "Numerics"); 1/z is staged per face
+        const float rs = rcp_nr(ws);
+        w0 = div_nr(w0, ws, rs);
+        w1 = div_nr(w1, ws, rs);
+        w2 = div_nr(w2, ws, rs);
+        const float sum = div_nr(w0, z0, q6.z) + div_nr(w1, z1, q6.w) + div_nr(w2, z2, q7.x);
+        if (in_range(sum, 0x1p-90f, 0x1p90f)) {
+            const float r = rcp_nr(sum);
+            zp = __builtin_fmaf(__builtin_fmaf(-sum, r, 1.f), r, r);  // div_nr(1, sum, r): 1 * r == r
+            zp = __builtin_fmaf(__builtin_fmaf(-sum, zp, 1.f), r, zp);
+        } else {
+            zp = 1.f / sum;
+        }
+    } else {
+        w0 /= ws;
+        w1 /= ws;
+        w2 /= ws;
+        zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
+    }
     if (zp <= near || far <= zp) return;
     if (zp <= depth_min - delta) {  // .cu:145-148
         depth_min = zp;
@@ -530,7 +590,11 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
     e[3] = make_float4(x2, y2, z0, z1);
     e[4] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
     e[5] = make_float4(y2 - y1, x0 - x2, y0 - y2, x1 * y2 - x2 * y1);
-    e[6] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, 0.f, 0.f);
+    e[6] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, rcp_nr(z0), rcp_nr(z1));
+    const bool ok = coord_ok(x0) && coord_ok(y0) && coord_ok(x1) && coord_ok(y1) && coord_ok(x2) && coord_ok(y2) &&
+                    in_range(z0, 0x1p-20f, 0x1p20f) && in_range(z1, 0x1p-20f, 0x1p20f) &&
+                    in_range(z2, 0x1p-20f, 0x1p20f);
+    e[7] = make_float4(rcp_nr(z2), 0.f, 0.f, __int_as_float(ok ? 1 : 0));
 }
 
 __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, const int2* __restrict__ bbox,
@@ -539,7 +603,8 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[FWD_LDS];
     __shared__ int s_scan[4];
     float4(*s_face)[FREC] = reinterpret_cast<float4(*)[FREC]>(s_raw);
-    int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
+    float4* s_box = reinterpret_cast<float4*>(s_raw + FCAP * FREC * 16);  // float bbox, conflict-free per-lane reads
+    int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16 + FCAP * 16);
 
     const int b = blockIdx.y;
     const int S = g.S;
@@ -550,22 +615,23 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
     const int by0 = bin_y * COARSE;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
-    int lx, ly;
-    pixel_of(t, lx, ly);
-    const int px = bx0 + lx;
-    const float xp = pix_center(px, S);
-    float yp[NSUB];
+    int lx[NSUB], ly[NSUB], ox[NSUB], oy[NSUB];
+    float xp[NSUB], yp[NSUB];
     float depth_min[NSUB];
     int best[NSUB];
+    float xcl[NSUB], xch[NSUB], ycl[NSUB], ych[NSUB];
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
-        yp[k] = pix_center(by0 + TH * k + ly, S);
+        pixel_of(t, k, lx[k], ly[k], ox[k], oy[k]);
+        xcl[k] = pix_center(bx0 + ox[k], S);
+        xch[k] = pix_center(bx0 + ox[k] + WBW - 1, S);
+        ycl[k] = pix_center(by0 + oy[k], S);
+        ych[k] = pix_center(by0 + oy[k] + WBH - 1, S);
+        xp[k] = pix_center(bx0 + lx[k], S);
+        yp[k] = pix_center(by0 + ly[k], S);
         depth_min[k] = far;
         best[k] = -1;
     }
-    // this wave's 16x4 pixel block in sub-tile 0 (sub-tile k adds TH * k to y)
-    const int wx0 = bx0 + (wid & 1) * 16, wx1 = wx0 + 15;
-    const int wy0 = by0 + (wid >> 1) * 4;
 
     const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
     const int2* bbb = bbox + (long long)b * F;
@@ -591,22 +657,23 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
                 if (t < n) {
                     const int f = s_cand[j0 + t];
                     stage_face(s_face[t], frb + (long long)f * 9, f, bbb[f]);
+                    s_box[t] = s_face[t][0];
                 }
                 __syncthreads();
 #pragma unroll
                 for (int k = 0; k < NSUB; k++) {
-                    const int y0w = wy0 + TH * k, y1w = y0w + 3;
+                    // pixel-centre extent of this wave's block: a face whose float bounding box
+                    // misses it fails .cu:94-97 at every pixel of the block
+                    const float xc0 = xcl[k], xc1 = xch[k], yc0 = ycl[k], yc1 = ych[k];
                     for (int c0 = 0; c0 < n; c0 += 64) {
                         bool hit = false;
                         if (c0 + lane < n) {
-                            const float4 q1 = s_face[c0 + lane][1];
-                            const int fbx = __float_as_int(q1.x), fby = __float_as_int(q1.y);
-                            hit = range_lo(fbx) <= wx1 && range_hi(fbx) >= wx0 && range_lo(fby) <= y1w &&
-                                  range_hi(fby) >= y0w;
+                            const float4 q0 = s_box[c0 + lane];
+                            hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
                         }
                         // faces touching this wave's pixels, walked in ascending order
                         for (unsigned long long m = __ballot(hit); m; m &= m - 1)
-                            face_test(s_face[c0 + __builtin_ctzll(m)], xp, yp[k], near, far, delta, depth_min[k],
+                            face_test(s_face[c0 + __builtin_ctzll(m)], xp[k], yp[k], near, far, delta, depth_min[k],
                                       best[k]);
                     }
                 }
@@ -617,7 +684,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
 
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
-        const int py = by0 + TH * k + ly;
+        const int px = bx0 + lx[k], py = by0 + ly[k];
         if (px < S && py < S) fim[((long long)b * S + py) * S + px] = best[k];
     }
 }

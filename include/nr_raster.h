@@ -106,8 +106,8 @@ typedef struct NrRasterArgs {
     long long tex_stride_b, tex_stride_c, tex_stride_p; /* p = flat texel index h * W + w */
     int tex_height, tex_width;
     /* saved state, written by forward, read by backward */
-    float* face_records;     /* [B, F, 9]: gathered faces (rasterize.py:232) */
-    float* face_uv;          /* [Buv, F, 6] with Buv = (vt_batch_stride ? B : 1); only with RGB */
+    float* face_records;     /* [B, F, 16]: gathered faces (rasterize.py:232) + per-face reciprocals/flags */
+    float* face_uv;          /* [Buv, F, 8] with Buv = (vt_batch_stride ? B : 1); only with RGB */
     int32_t* face_index;     /* [B, S, S] */
     void* workspace;         /* forward scratch, nr_workspace_bytes(B, F, S) */
     size_t workspace_bytes;
@@ -115,6 +115,10 @@ typedef struct NrRasterArgs {
      * vertex_faces[vertex_offsets[v] .. vertex_offsets[v+1]) lists 3 f + k for every faces[f, k] == v. */
     const int32_t* vertex_offsets; /* [V + 1] */
     const int32_t* vertex_faces;   /* [3 F] */
+    /* optional halo cache, nr_halo_bytes() bytes: when set, the forward stores the internal-image
+     * values of the backward's tile borders there and the backward reads them instead of shading
+     * its tile halos again; NULL = backward re-shades (same results). */
+    float* halo;
 } NrRasterArgs;
 
 /* Channels in output order: rgb (3), silhouettes (1), depth (1) -- those enabled by draw_flags. */
@@ -122,6 +126,9 @@ NR_API int nr_num_channels(int draw_flags);
 
 /* rasterize.py:194-329 (without lights / backgrounds): images [B, C, s, s] contiguous. */
 NR_API int nr_rasterize_forward(const NrRasterArgs* args, float* images, void* stream);
+
+/* Bytes of NrRasterArgs.halo for B items at output size s (internal 2s with anti-aliasing). */
+NR_API size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw_flags);
 
 /* Scratch bytes of nr_rasterize_backward: per-face gradient records [B, F, 9] and the texture
  * gradient accumulator [texture_items, H*W rounded up to 4, 4]. */
@@ -134,6 +141,12 @@ NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int tex
  * (the batch total when the textures are shared).  Needs args->vertex_offsets/vertex_faces. */
 NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
                                  float* grad_textures, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Diagnostics (no reference counterpart): the kernels replace some IEEE divisions by a shortened
+ * form of the compiler's own division sequence inside a guarded operand range (DESIGN.md,
+ * "Numerics").  This runs both forms on n operand pairs so tests can check they agree bit for bit. */
+NR_API int nr_selftest_division(const float* a, const float* b, float* q_fast, float* q_ieee, long long n,
+                                void* stream);
 
 /* Measurement hook (bench.py's roofline leg; no reference counterpart).  With profiling on, the
  * library brackets each launch of its kernels with a pair of HIP events recorded on the launch

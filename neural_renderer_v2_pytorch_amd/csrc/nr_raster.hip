@@ -132,8 +132,18 @@ __device__ __forceinline__ int pack_range(int lo, int hi) { return (lo & 0xffff)
 __device__ __forceinline__ int range_lo(int p) { return p & 0xffff; }
 __device__ __forceinline__ int range_hi(int p) { return p >> 16; }
 
+// A gathered face.  The fused path keeps 16-float face records (FACE_REC floats, 64 B, one aligned
+// load of 4 x float4): the 9 corner coordinates, then per-face reciprocals for the exact division
+// shortcut (rcp_nr(z_k), rcp_nr(z_k + 1e-10)) and the operand-range flags that allow it.  Faces
+// handed over by the caller (face_index_map_forward_safe, compute_weight_map) are 9 floats and
+// always take the plain IEEE divisions (flags = 0).
+constexpr int FACE_REC = 16;
+constexpr int FACE_FAST_XYZ = 1;  // x, y in {0} u [2^-20, 2^20], |z| in [2^-20, 2^20]
+constexpr int FACE_FAST_ZQ = 2;   // |z + 1e-10| in [2^-20, 2^20]
 struct Face {
     float x0, y0, z0, x1, y1, z1, x2, y2, z2;
+    float rz0, rz1, rz2, rq0, rq1, rq2;
+    int flags;
 };
 
 __device__ __forceinline__ Face load_face(const float* __restrict__ fr) {
@@ -141,6 +151,26 @@ __device__ __forceinline__ Face load_face(const float* __restrict__ fr) {
     f.x0 = fr[0]; f.y0 = fr[1]; f.z0 = fr[2];
     f.x1 = fr[3]; f.y1 = fr[4]; f.z1 = fr[5];
     f.x2 = fr[6]; f.y2 = fr[7]; f.z2 = fr[8];
+    f.rz0 = f.rz1 = f.rz2 = f.rq0 = f.rq1 = f.rq2 = 0.f;
+    f.flags = 0;
+    return f;
+}
+
+__device__ __forceinline__ Face load_face_rec(const float* __restrict__ fr) {
+    const float4* p = reinterpret_cast<const float4*>(fr);
+    const float4 a = p[0], b = p[1], c = p[2], d = p[3];
+    Face f;
+    f.x0 = a.x; f.y0 = a.y; f.z0 = a.z;
+    f.x1 = a.w; f.y1 = b.x; f.z1 = b.y;
+    f.x2 = b.z; f.y2 = b.w; f.z2 = c.x;
+    f.rz0 = c.y; f.rz1 = c.z; f.rz2 = c.w;
+    f.rq0 = d.x; f.rq1 = d.y; f.rq2 = d.z;
+    f.flags = __float_as_int(d.w);
+    return f;
+}
+
+__device__ __forceinline__ Face empty_face() {
+    Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     return f;
 }
 
@@ -172,8 +202,10 @@ __device__ __forceinline__ bool in_range(float x, float lo, float hi) { return f
 // coordinate / depth magnitudes for which the face-level guard below holds: 0 or [2^-20, 2^20]
 __device__ __forceinline__ bool coord_ok(float x) { return x == 0.f || in_range(x, 0x1p-20f, 0x1p20f); }
 
-// compute_weight_map_cuda_kernel (.cu:286-306)
-__device__ __forceinline__ void face_weights(float xp, float yp, const Face& f, float w[3]) {
+// compute_weight_map_cuda_kernel (.cu:286-306).  Returns true when the weights are known to lie in
+// {0} u [2^-84, 1] (the exact-division path was taken), which the texture and depth stages below
+// need for their own shortcut.
+__device__ __forceinline__ bool face_weights(float xp, float yp, const Face& f, float w[3]) {
     w[0] = yp * (f.x2 - f.x1) + xp * (f.y1 - f.y2) + (f.x1 * f.y2 - f.x2 * f.y1);
     w[1] = yp * (f.x0 - f.x2) + xp * (f.y2 - f.y0) + (f.x2 * f.y0 - f.x0 * f.y2);
     w[2] = yp * (f.x1 - f.x0) + xp * (f.y0 - f.y1) + (f.x0 * f.y1 - f.x1 * f.y0);
@@ -187,8 +219,26 @@ __device__ __forceinline__ void face_weights(float xp, float yp, const Face& f, 
     w[1] = fmaxf(w[1], 0.f);
     w[2] = fmaxf(w[2], 0.f);
     s = w[0] + w[1] + w[2];
+    // with FACE_FAST_XYZ every w is 0 or in [2^-80, 2^42] (DESIGN.md "Numerics")
+    if ((f.flags & FACE_FAST_XYZ) && in_range(s, 0x1p-20f, 0x1p4f)) {
+        const float r = rcp_nr(s);
+#pragma unroll
+        for (int j = 0; j < 3; j++) w[j] = fmaxf(fminf(div_nr(w[j], s, r), 1.f), 0.f);
+        return true;
+    }
 #pragma unroll
     for (int j = 0; j < 3; j++) w[j] = fmaxf(fminf(w[j] / s, 1.f), 0.f);
+    return false;
+}
+
+// 1 / x through div_nr's range (|x| in [2^-90, 2^90]), else IEEE
+__device__ __forceinline__ float recip_exact(float x) {
+    if (in_range(x, 0x1p-90f, 0x1p90f)) {
+        const float r = rcp_nr(x);
+        const float q = __builtin_fmaf(__builtin_fmaf(-x, r, 1.f), r, r);  // div_nr(1, x, r): 1 * r == r
+        return __builtin_fmaf(__builtin_fmaf(-x, q, 1.f), r, q);
+    }
+    return 1.f / x;
 }
 
 struct TexView {
@@ -217,21 +267,31 @@ struct TexSample {
     float rgb[3];
 };
 
-__device__ __forceinline__ void sample_texture(const Face& f, const float w[3], const float* __restrict__ uv,
+// uv: the face's 8-float texture record (u0 v0 u1 v1 u2 v2, flag, -); flag 1 = every u, v in
+// {0} u [2^-16, 2^20].  wfast: face_weights took its exact-division path.
+__device__ __forceinline__ void sample_texture(const Face& f, const float w[3], bool wfast, const float* __restrict__ uv,
                                                const TexView& tv, int bt, float eps, TexSample& s) {
+    const float4 uva = reinterpret_cast<const float4*>(uv)[0], uvb = reinterpret_cast<const float4*>(uv)[1];
+    const float uvs[6] = {uva.x, uva.y, uva.z, uva.w, uvb.x, uvb.y};
+    const bool fast = wfast && (f.flags & FACE_FAST_ZQ) && __float_as_int(uvb.z) != 0;
     const float z[3] = {f.z0, f.z1, f.z2};
+    const float rq[3] = {f.rq0, f.rq1, f.rq2};
     float st = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         s.zq[k] = z[k] + 1e-10f;
-        const float t = w[k] / s.zq[k] + 1e-10f;
+        const float t = (fast ? div_nr(w[k], s.zq[k], rq[k]) : w[k] / s.zq[k]) + 1e-10f;
         st = (k == 0) ? t : st + t;
     }
-    s.dt = 1.f / st;
+    s.dt = fast ? recip_exact(st) : 1.f / st;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
-        const float u0 = uv[j], u1 = uv[2 + j], u2 = uv[4 + j];
-        s.num[j] = ((w[0] * u0) / s.zq[0] + (w[1] * u1) / s.zq[1]) + (w[2] * u2) / s.zq[2];
+        const float u0 = uvs[j], u1 = uvs[2 + j], u2 = uvs[4 + j];
+        if (fast)
+            s.num[j] = (div_nr(w[0] * u0, s.zq[0], rq[0]) + div_nr(w[1] * u1, s.zq[1], rq[1])) +
+                       div_nr(w[2] * u2, s.zq[2], rq[2]);
+        else
+            s.num[j] = ((w[0] * u0) / s.zq[0] + (w[1] * u1) / s.zq[1]) + (w[2] * u2) / s.zq[2];
         s.pr[j] = s.num[j] * s.dt;
         s.lo[j] = t_min(t_min(u0, u1), u2);
         s.hm[j] = t_max(t_max(u0, u1), u2) - eps;
@@ -264,7 +324,10 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
 }
 
 // compute_depth_map (rasterize.py:80-88) for a foreground pixel
-__device__ __forceinline__ float depth_value(const Face& f, const float w[3]) {
+__device__ __forceinline__ float depth_value(const Face& f, const float w[3], bool wfast) {
+    if (wfast) {  // weights in {0} u [2^-84, 1], |z| in [2^-20, 2^20]
+        return recip_exact((div_nr(w[0], f.z0, f.rz0) + div_nr(w[1], f.z1, f.rz1)) + div_nr(w[2], f.z2, f.rz2));
+    }
     return 1.f / ((w[0] / f.z0 + w[1] / f.z1) + w[2] / f.z2);
 }
 
@@ -274,7 +337,7 @@ struct Shade {
     float eps;
     TexView tv;
     const float* __restrict__ face_uv;
-    long long uv_bstride;  // F*6 or 0
+    long long uv_bstride;  // F*8 or 0
 };
 
 // All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth), written
@@ -285,17 +348,17 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
     float r = 0.f, gg = 0.f, bb = 0.f, sil = 0.f, dep = 0.f;
     if (fi >= 0) {
         float w[3];
-        face_weights(xp, yp, f, w);
+        const bool wfast = face_weights(xp, yp, f, w);
         if (R) {
             TexSample s;
-            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 6;
-            sample_texture(f, w, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s);
+            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 8;
+            sample_texture(f, w, wfast, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s);
             r = s.rgb[0];
             gg = s.rgb[1];
             bb = s.rgb[2];
         }
         sil = 1.f;
-        if (sh.draw & NR_DRAW_DEPTH) dep = depth_value(f, w);
+        if (sh.draw & NR_DRAW_DEPTH) dep = depth_value(f, w, wfast);
     }
     out[0] = R ? r : (Sl ? sil : dep);
     out[1] = R ? gg : dep;
@@ -407,7 +470,6 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         int2 bb = make_int2(NR_EMPTY_RANGE, NR_EMPTY_RANGE);
         if (f < F) {
             float c[9];
-            float* rec = face_records + ((long long)b * F + f) * 9;
             if (GATHER) {
                 const float* vb = vertices + (long long)b * V * 3;
 #pragma unroll
@@ -417,9 +479,26 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                     c[3 * k + 1] = vb[vi * 3 + 1];
                     c[3 * k + 2] = vb[vi * 3 + 2];
                 }
+                // 16-float record: corners, rcp_nr(z_k), rcp_nr(z_k + 1e-10), range flags (see Face)
+                bool fxyz = true, fzq = true;
 #pragma unroll
-                for (int k = 0; k < 9; k++) rec[k] = c[k];
+                for (int k = 0; k < 3; k++) {
+                    fxyz = fxyz && coord_ok(c[3 * k]) && coord_ok(c[3 * k + 1]) && in_range(c[3 * k + 2], 0x1p-20f, 0x1p20f);
+                    fzq = fzq && in_range(c[3 * k + 2] + 1e-10f, 0x1p-20f, 0x1p20f);
+                }
+#ifdef NR_NO_FASTDIV
+                const int flags = 0;  // timing build: IEEE divisions everywhere
+#else
+                const int flags = (fxyz ? FACE_FAST_XYZ : 0) | (fzq ? FACE_FAST_ZQ : 0);
+#endif
+                float4* rec = reinterpret_cast<float4*>(face_records + ((long long)b * F + f) * FACE_REC);
+                rec[0] = make_float4(c[0], c[1], c[2], c[3]);
+                rec[1] = make_float4(c[4], c[5], c[6], c[7]);
+                rec[2] = make_float4(c[8], rcp_nr(c[2]), rcp_nr(c[5]), rcp_nr(c[8]));
+                rec[3] = make_float4(rcp_nr(c[2] + 1e-10f), rcp_nr(c[5] + 1e-10f), rcp_nr(c[8] + 1e-10f),
+                                     __int_as_float(flags));
             } else {
+                const float* rec = face_records + ((long long)b * F + f) * 9;  // caller's [B, F, 3, 3]
 #pragma unroll
                 for (int k = 0; k < 9; k++) c[k] = rec[k];
             }
@@ -439,13 +518,20 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
             }
             if (face_uv != nullptr && b < uv_items) {
                 const float* vtb = vt + (long long)b * vt_bstride;
-                float* u = face_uv + ((long long)b * F + f) * 6;
+                float uv[6];
+                bool uok = true;
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
                     const int ti = faces_t[f * 3 + k];
-                    u[2 * k + 0] = vtb[(long long)ti * 2 + 0];
-                    u[2 * k + 1] = vtb[(long long)ti * 2 + 1];
+                    uv[2 * k + 0] = vtb[(long long)ti * 2 + 0];
+                    uv[2 * k + 1] = vtb[(long long)ti * 2 + 1];
                 }
+#pragma unroll
+                for (int k = 0; k < 6; k++) uok = uok && (uv[k] == 0.f || in_range(uv[k], 0x1p-16f, 0x1p20f));
+                // 8-float texture record: u0 v0 u1 v1 u2 v2, range flag (see sample_texture), pad
+                float4* u = reinterpret_cast<float4*>(face_uv + ((long long)b * F + f) * 8);
+                u[0] = make_float4(uv[0], uv[1], uv[2], uv[3]);
+                u[1] = make_float4(uv[4], uv[5], __int_as_float(uok ? 1 : 0), 0.f);
             }
             bbox[(long long)b * F + f] = bb;
         }
@@ -597,9 +683,10 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
     e[7] = make_float4(rcp_nr(z2), 0.f, 0.f, __int_as_float(ok ? 1 : 0));
 }
 
-__global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, const int2* __restrict__ bbox,
-                                                  const uint32_t* __restrict__ mask, int F, Geom g, float near,
-                                                  float far, float delta, int32_t* __restrict__ fim) {
+__global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, int rs,
+                                                  const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
+                                                  int F, Geom g, float near, float far, float delta,
+                                                  int32_t* __restrict__ fim) {
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[FWD_LDS];
     __shared__ int s_scan[4];
     float4(*s_face)[FREC] = reinterpret_cast<float4(*)[FREC]>(s_raw);
@@ -635,7 +722,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
 
     const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
     const int2* bbb = bbox + (long long)b * F;
-    const float* frb = face_records + (long long)b * F * 9;
+    const float* frb = face_records + (long long)b * F * rs;
 
     for (int wbase = 0; wbase < g.nwords; wbase += NT) {
         const int w = wbase + t;
@@ -656,7 +743,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
                 const int n = min(FCAP, nc - j0);
                 if (t < n) {
                     const int f = s_cand[j0 + t];
-                    stage_face(s_face[t], frb + (long long)f * 9, f, bbb[f]);
+                    stage_face(s_face[t], frb + (long long)f * rs, f, bbb[f]);
                     s_box[t] = s_face[t][0];
                 }
                 __syncthreads();
@@ -690,13 +777,61 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
 }
 
 // ------------------------------------------------------------------------------------------------
+// Halo cache: the internal-image values of the pixels on the border rows / columns of the backward's
+// 32x16 tiles, written by k_shade (which computes every internal pixel anyway) so that
+// k_raster_bwd loads its 1-pixel tile halo (asynchronously, during its main work) instead of
+// re-shading it.  Per item:
+//   rows: [nty][2][C][S]        side 0 = row 16 ty, side 1 = row 16 ty + 15, every column
+//   cols: [nty][C][16][ntx][2]  row y = 16 ty + r of column 32 tx (side 0) / 32 tx + 31 (side 1)
+// Both parts are written in contiguous runs by a shade block (one output row = two internal rows).
+constexpr int HALO_TW = 32, HALO_TH = 16;
+__host__ __device__ __forceinline__ long long halo_item_floats(int S, int C) {
+    const long long nty = (S + HALO_TH - 1) / HALO_TH, ntx = (S + HALO_TW - 1) / HALO_TW;
+    return nty * 2 * C * (long long)S + nty * C * HALO_TH * ntx * 2;
+}
+__device__ __forceinline__ int halo_row_offset(int C, int S, int x, int y, int c) {
+    return (((y / HALO_TH) * 2 + ((y & (HALO_TH - 1)) != 0)) * C + c) * S + x;
+}
+__device__ __forceinline__ int halo_col_offset(int C, int S, int x, int y, int c) {
+    const int nty = (S + HALO_TH - 1) / HALO_TH, ntx = (S + HALO_TW - 1) / HALO_TW;
+    return nty * 2 * C * S + (((y / HALO_TH) * C + c) * HALO_TH + (y & (HALO_TH - 1))) * (2 * ntx) +
+           2 * (x / HALO_TW) + ((x & (HALO_TW - 1)) != 0);
+}
+// offset of channel 0 of tile-border pixel (x, y) and the stride between its channels
+__device__ __forceinline__ void halo_locate(int C, int S, int x, int y, int& off, int& cstride) {
+    const int ry = y & (HALO_TH - 1);
+    if (ry == 0 || ry == HALO_TH - 1) {
+        off = halo_row_offset(C, S, x, y, 0);
+        cstride = S;
+    } else {
+        off = halo_col_offset(C, S, x, y, 0);
+        cstride = HALO_TH * 2 * ((S + HALO_TW - 1) / HALO_TW);
+    }
+}
+__device__ __forceinline__ void halo_store(float* __restrict__ halo, int b, int C, int S, int x, int y, const float* v) {
+    float* base = halo + b * halo_item_floats(S, C);
+    const int ry = y & (HALO_TH - 1), rx = x & (HALO_TW - 1);
+    if (ry == 0 || ry == HALO_TH - 1) {
+#pragma unroll
+        for (int c = 0; c < MAXC; c++)
+            if (c < C) base[halo_row_offset(C, S, x, y, c)] = v[c];
+    }
+    if (rx == 0 || rx == HALO_TW - 1) {
+#pragma unroll
+        for (int c = 0; c < MAXC; c++)
+            if (c < C) base[halo_col_offset(C, S, x, y, c)] = v[c];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_shade: the image channels from the face-index map, one thread per OUTPUT pixel (rasterize.py:
 // 237-328): weights (compute_weight_map), texture sample, silhouette and depth for the 1 or 2x2
 // internal pixels it covers, merged in rgb/sil/depth order, flipped, and 2x2-averaged with the
 // reference's summation order.  Kept out of the rasteriser so that kernel stays lean (registers,
 // occupancy); costs one extra read of the face-index map.
 __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
-                                               int F, int S, Shade sh, int aa, float* __restrict__ images) {
+                                               int F, int S, Shade sh, int aa, float* __restrict__ images,
+                                               float* __restrict__ halo) {
     const int s = aa ? S / 2 : S;
     const int b = blockIdx.y;
     int blk = blockIdx.x, unused;
@@ -704,20 +839,21 @@ __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_re
     const int o = blk * blockDim.x + threadIdx.x;
     if (o >= s * s) return;
     const int oi = o / s, oj = o - oi * s;
-    const float* frb = face_records + (long long)b * F * 9;
+    const float* frb = face_records + (long long)b * F * FACE_REC;
     const int32_t* fb = fim + (long long)b * S * S;
     float* ob = images + (long long)b * sh.C * s * s + o;
     if (!aa) {
         // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
         const int y = S - 1 - oi, x = S - 1 - oj;
         const int fi = fb[(long long)y * S + x];
-        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (fi >= 0) f = load_face(frb + (long long)fi * 9);
+        Face f = empty_face();
+        if (fi >= 0) f = load_face_rec(frb + (long long)fi * FACE_REC);
         float v[MAXC];
         shade_pixel(sh, b, fi, f, pix_center(x, S), pix_center(y, S), v);
 #pragma unroll
         for (int c = 0; c < MAXC; c++)
             if (c < sh.C) ob[(long long)c * s * s] = v[c];
+        if (halo) halo_store(halo, b, sh.C, S, x, y, v);
         return;
     }
     // 2x2 average of the flipped image (rasterize.py:321-328): output (oi, oj) reads internal rows
@@ -730,13 +866,38 @@ __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_re
     float v[4][MAXC];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (fis[q] >= 0) f = load_face(frb + (long long)fis[q] * 9);
+        Face f = empty_face();
+        if (fis[q] >= 0) f = load_face_rec(frb + (long long)fis[q] * FACE_REC);
         shade_pixel(sh, b, fis[q], f, pix_center(xs[q], S), pix_center(ys[q], S), v[q]);
     }
 #pragma unroll
     for (int c = 0; c < MAXC; c++)
         if (c < sh.C) ob[(long long)c * s * s] = (((v[0][c] + v[1][c]) + v[2][c]) + v[3][c]) / 4.f;
+    if (halo) {
+        // this thread's 2x2 internal pixels on the backward's tile borders: rows iy (top border) /
+        // iy + 1 (bottom border) as float2 pairs, columns ix (left) / ix + 1 (right)
+        float* hb = halo + b * halo_item_floats(S, sh.C);
+        const int C = sh.C;
+        const int ry = iy & (HALO_TH - 1), rx = ix & (HALO_TW - 1);
+        if (ry == 0 || ry == HALO_TH - 2) {
+            const int top = ry == 0, y = top ? iy : iy + 1;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++)
+                if (c < C)
+                    *reinterpret_cast<float2*>(hb + halo_row_offset(C, S, ix, y, c)) =
+                        top ? make_float2(v[3][c], v[1][c]) : make_float2(v[2][c], v[0][c]);
+        }
+        if (rx == 0 || rx == HALO_TW - 2) {
+            const int left = rx == 0, x = left ? ix : ix + 1;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                if (c < C) {
+                    hb[halo_col_offset(C, S, x, iy, c)] = left ? v[3][c] : v[1][c];
+                    hb[halo_col_offset(C, S, x, iy + 1, c)] = left ? v[2][c] : v[0][c];
+                }
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -867,12 +1028,17 @@ constexpr int TWIN = 4;                       // texel window edge per face
 constexpr int REC = 20;                       // staged record: ay by ax bx | pos G_rgb[3] | gF[9] | pad
 constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
 constexpr int BWD_LDS_REC = 4 * 128 * REC * 4;
-constexpr int BWD_LDS = BWD_LDS_IG > BWD_LDS_REC ? BWD_LDS_IG : BWD_LDS_REC;
+constexpr int BWD_LDS_HALO = 2 * MAXC * 128 * 4;  // halo staging (step 0), after the I / G planes
+constexpr int BWD_LDS = BWD_LDS_IG + BWD_LDS_HALO > BWD_LDS_REC ? BWD_LDS_IG + BWD_LDS_HALO : BWD_LDS_REC;
+static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 // experiment switch for timing builds (never set in the shipped library):
 //   2 = no gradient accumulation (steps 3 and 4), 4 = no global atomics (step 4),
-//   8 = no per-face gather (step 3's member loop)
+//   8 = no per-face gather (step 3's member loop), 16 = no halo shading, 64 = no stencil
 #ifndef NR_ABLATE
 #define NR_ABLATE 0
+#endif
+#ifndef NR_HALO_EARLY
+#define NR_HALO_EARLY 1
 #endif
 
 struct BwdArgs {
@@ -881,6 +1047,7 @@ struct BwdArgs {
     const float* __restrict__ grad_images;
     float* __restrict__ grad_faces;   // [B, F, 9]
     float* __restrict__ grad_tex4;    // [Bt, HWp, 4] or null
+    const float* __restrict__ halo;   // halo cache written by the forward, or null (re-shade the halo)
     int F, aa, s, HWp;
     float step, inv_step;
     int step_pow2;                     // x / step == x * inv_step exactly
@@ -922,6 +1089,15 @@ __device__ __forceinline__ float stencil(const BwdArgs& a, const float* Im, cons
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+// position (hy, hx) in the (BH + 2) x (TW + 2) tile frame of halo pixel t < NHALO: top row, bottom
+// row, left column, right column
+__device__ __forceinline__ void halo_pixel(int t, int& hy, int& hx) {
+    if (t < HW_) { hy = 0; hx = t; }
+    else if (t < 2 * HW_) { hy = HH_ - 1; hx = t - HW_; }
+    else if (t < 2 * HW_ + BH) { hy = 1 + (t - 2 * HW_); hx = 0; }
+    else { hy = 1 + (t - 2 * HW_ - BH); hx = HW_ - 1; }
+}
+
 // per interior pixel state carried across the stencil's barrier
 struct BwdPix {
     int fi;            // face index (-1: background or outside)
@@ -933,7 +1109,7 @@ struct BwdPix {
     int wx, wy;        // face window origin (texels); INT_MIN when not windowed
 };
 
-__global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) {
     __shared__ __attribute__((aligned(16))) float s_raw[BWD_LDS / 4];
     float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
     float(*s_G)[HN] = reinterpret_cast<float(*)[HN]>(s_raw + MAXC * HN);
@@ -954,6 +1130,37 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
     const int ly0 = (wid >> 1) * 8 + (lane >> 4);
     const int px = tx0 + lx;
     const float xp = pix_center(px, S);
+
+    // halo ring from the forward's halo cache: asynchronous global -> LDS loads by waves 0 and 1
+    // (lane t < NHALO carries halo pixel t, ring order of halo_pixel), landed before the barrier
+    float(*s_hI)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4);
+    float(*s_hG)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4 + MAXC * 128);
+    auto halo_prefetch = [&]() {
+        if (a.halo && t < 128) {
+            int hy, hx;
+            halo_pixel(t, hy, hx);
+            const int hpy = ty0 - 1 + hy, hpx = tx0 - 1 + hx;
+            const bool h_in = t < NHALO && hpy >= 0 && hpy < S && hpx >= 0 && hpx < S;
+            int hoff = 0, hcs = 0;
+            if (h_in) halo_locate(C, S, hpx, hpy, hoff, hcs);
+            const float* hsrc = a.halo + b * halo_item_floats(S, C) + hoff;
+            const float* gsrc = a.grad_images + (long long)b * C * (a.aa ? a.s * a.s : S * S);
+            if (h_in) gsrc += a.aa ? ((S - 1 - hpy) >> 1) * a.s + ((S - 1 - hpx) >> 1) : (S - 1 - hpy) * S + (S - 1 - hpx);
+            const int gplane = a.aa ? a.s * a.s : S * S;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                if (c < C) {
+                    __builtin_amdgcn_global_load_lds((const void*)(hsrc + c * hcs),
+                                                     (void __attribute__((address_space(3)))*)(&s_hI[c][wid * 64]), 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void*)(gsrc + (long long)c * gplane),
+                                                     (void __attribute__((address_space(3)))*)(&s_hG[c][wid * 64]), 4, 0, 0);
+                }
+            }
+        }
+    };
+#if NR_HALO_EARLY
+    halo_prefetch();  // in flight during step 1
+#endif
 
     // ---- 1. image + upstream gradient (LDS), and the stencil-independent gradient terms ---------
     BwdPix P[2];
@@ -981,14 +1188,17 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         if (q.fi < 0) continue;
         const float yp = pix_center(py, S);
         const float* G = G2[k];
-        const Face f = load_face(a.face_records + ((long long)b * a.F + q.fi) * 9);
-        face_weights(xp, yp, f, q.w);
+        Face f = load_face_rec(a.face_records + ((long long)b * a.F + q.fi) * FACE_REC);
+#ifndef NR_BWD_FASTDIV
+        f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
+#endif
+        const bool wfast = face_weights(xp, yp, f, q.w);
         const float* w = q.w;
         float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
         if (rgb) {
             TexSample s;
-            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)q.fi * 6;
-            sample_texture(f, w, fuv, sh.tv, bt, sh.eps, s);
+            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)q.fi * 8;
+            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s);
             r = s.rgb[0];
             gg = s.rgb[1];
             bb = s.rgb[2];
@@ -1079,7 +1289,7 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
             }
         }
         if (sh.draw & NR_DRAW_DEPTH) {
-            dep = depth_value(f, w);
+            dep = depth_value(f, w, wfast);
             // depth channel gradient reloaded (cache hit) rather than a runtime-indexed register array
             const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
             const float gd = upstream_one(a, C, b, py, px, S, dc);
@@ -1110,23 +1320,37 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
             }
         }
     }
+#if !NR_HALO_EARLY
+    halo_prefetch();
+#endif
     // halo ring: image and upstream gradient only
-    if (t < NHALO) {
-        int hy, hx;
-        if (t < HW_) { hy = 0; hx = t; }
-        else if (t < 2 * HW_) { hy = HH_ - 1; hx = t - HW_; }
-        else if (t < 2 * HW_ + BH) { hy = 1 + (t - 2 * HW_); hx = 0; }
-        else { hy = 1 + (t - 2 * HW_ - BH); hx = HW_ - 1; }
-        const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+    int hy, hx;
+    halo_pixel(t, hy, hx);
+    const int hpy = ty0 - 1 + hy, hpx = tx0 - 1 + hx;
+    const bool h_in = t < NHALO && hpy >= 0 && hpy < S && hpx >= 0 && hpx < S;
+    if (a.halo) {
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMA halo loads have landed
+        __syncthreads();
+        if (t < NHALO) {
+            const int hl = hy * HW_ + hx;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                if (c < C) {
+                    s_I[c][hl] = h_in ? s_hI[c][t] : 0.f;
+                    s_G[c][hl] = h_in ? (a.aa ? s_hG[c][t] / 4.f : s_hG[c][t]) : 0.f;
+                }
+            }
+        }
+    } else if (t < NHALO) {
         float hI[MAXC], hG[MAXC];
 #pragma unroll
         for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
-        if (y >= 0 && y < S && x >= 0 && x < S) {
-            const int hf = a.fim[((long long)b * S + y) * S + x];
-            Face ff = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            if (hf >= 0) ff = load_face(a.face_records + ((long long)b * a.F + hf) * 9);
-            shade_pixel(sh, b, hf, ff, pix_center(x, S), pix_center(y, S), hI);
-            upstream_grad(a, C, b, y, x, S, hG);
+        if (!(NR_ABLATE & 16) && h_in) {
+            const int hf = a.fim[((long long)b * S + hpy) * S + hpx];
+            Face ff = empty_face();
+            if (hf >= 0) ff = load_face_rec(a.face_records + ((long long)b * a.F + hf) * FACE_REC);
+            shade_pixel(sh, b, hf, ff, pix_center(hpx, S), pix_center(hpy, S), hI);
+            upstream_grad(a, C, b, hpy, hpx, S, hG);
         }
         const int hl = hy * HW_ + hx;
 #pragma unroll
@@ -1149,21 +1373,23 @@ __global__ __launch_bounds__(NT) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) 
         if (q.fi < 0) continue;
         const int py = ty0 + ly0 + 4 * k;
         const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
-        float Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
+        // centre values re-read from LDS (not kept in registers across the barrier)
+        float I0[MAXC], G0[MAXC], Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
             const bool u = c < C;
+            I0[c] = u ? s_I[c][li] : 0.f; G0[c] = u ? s_G[c][li] : 0.f;
             Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
             Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
         }
-        const float gx = stencil(a, Im, I2[k], Ip, Gm, G2[k], Gp, px, S, C);
+        const float gx = (NR_ABLATE & 64) ? Im[0] : stencil(a, Im, I0, Ip, Gm, G0, Gp, px, S, C);
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
             const bool u = c < C;
             Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
             Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
         }
-        const float gy = stencil(a, Im, I2[k], Ip, Gm, G2[k], Gp, py, S, C);
+        const float gy = (NR_ABLATE & 64) ? Ip[0] : stencil(a, Im, I0, Ip, Gm, G0, Gp, py, S, C);
         // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
 #pragma unroll
         for (int j = 0; j < 3; j++) {
@@ -1322,11 +1548,22 @@ Shade make_shade(const NrRasterArgs* a) {
     sh.tv.H = a->tex_height;
     sh.tv.W = a->tex_width;
     sh.face_uv = a->face_uv;
-    sh.uv_bstride = a->vt_batch_stride ? (long long)a->num_faces * 6 : 0;
+    sh.uv_bstride = a->vt_batch_stride ? (long long)a->num_faces * 8 : 0;
     return sh;
 }
 
 }  // namespace
+
+// self-test of the exact division shortcut (nr_selftest_division): q_fast = div_nr(a, b, rcp_nr(b)),
+// q_ieee = a / b as the compiler lowers it
+__global__ void k_selftest_div(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ qf,
+                               float* __restrict__ qi, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = a[i], y = b[i];
+    qf[i] = div_nr(x, y, rcp_nr(y));
+    qi[i] = x / y;
+}
 
 // ==================================================================================================
 extern "C" {
@@ -1370,8 +1607,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     }
     {
         ProfScope _p(P_RASTER, st);
-        hipLaunchKernelGGL(k_raster_fwd, dim3(g.nbins, B), dim3(NT), 0, st, face_records, bbox, mask, F, g, near, far,
-                           delta, fim);
+        hipLaunchKernelGGL(k_raster_fwd, dim3(g.nbins, B), dim3(NT), 0, st, face_records, vertices ? FACE_REC : 9, bbox, mask,
+                           F, g, near, far, delta, fim);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra) return e;
@@ -1379,7 +1616,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     {
         ProfScope _p(P_SHADE, st);
         hipLaunchKernelGGL(k_shade, dim3((unsigned)(((long long)s * s + 255) / 256), B), dim3(256), 0, st, face_records, fim,
-                           F, S, make_shade(ra), ra->anti_aliasing, images);
+                           F, S, make_shade(ra), ra->anti_aliasing, images, ra->halo);
     }
     return check_launch("k_shade");
 }
@@ -1443,6 +1680,12 @@ int nr_rasterize_forward(const NrRasterArgs* a, float* images, void* stream) {
                           a->workspace_bytes, (hipStream_t)stream, a, images);
 }
 
+size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw_flags) {
+    const int S = anti_aliasing ? 2 * image_size : image_size;
+    if (batch_size <= 0 || image_size <= 0) return 0;
+    return (size_t)batch_size * halo_item_floats(S, nr_num_channels(draw_flags)) * sizeof(float);
+}
+
 size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int texture_items, int tex_height,
                                    int tex_width) {
     const size_t hwp = ((size_t)tex_height * tex_width + 3) & ~size_t(3);
@@ -1477,6 +1720,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.grad_images = grad_images;
     ba.grad_faces = gF;
     ba.grad_tex4 = rgb ? g4 : nullptr;
+    ba.halo = a->halo;
     ba.F = a->num_faces;
     ba.aa = a->anti_aliasing;
     ba.s = a->image_size;
@@ -1511,6 +1755,14 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
         e = check_launch("k_tex_out");
     }
     return e;
+}
+
+int nr_selftest_division(const float* a, const float* b, float* q_fast, float* q_ieee, long long n, void* stream) {
+    if (n < 0 || (n > 0 && (!a || !b || !q_fast || !q_ieee))) return fail(NR_ERR_ARGS, "bad arguments");
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(k_selftest_div, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a, b,
+                       q_fast, q_ieee, n);
+    return check_launch("k_selftest_div");
 }
 
 int nr_profile_enable(int on) {

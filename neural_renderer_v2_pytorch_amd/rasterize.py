@@ -18,6 +18,8 @@ Behavioural notes ("Drop-in boundary"):
   * gradients flow to vertices and textures; a vertices_textures tensor that requires grad is
     rejected (NotImplementedError) rather than silently given no gradient.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -167,7 +169,7 @@ class _Cfg:
                  "tex_hw", "vt_shared", "Vt", "B", "tex_view")
 
 
-def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj=None):
+def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj=None, halo=None):
     a = _lib.NrRasterArgs()
     a.batch_size = cfg.B
     a.num_vertices = cfg.V
@@ -190,6 +192,8 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj
     else:  # the backward does not use the forward workspace
         a.workspace = None
         a.workspace_bytes = 0
+    if halo is not None:
+        a.halo = halo.data_ptr()
     if adj is not None:
         a.vertex_offsets = adj[0].data_ptr()
         a.vertex_faces = adj[1].data_ptr()
@@ -206,6 +210,11 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj
     return a
 
 
+# the forward stores the backward's tile-border image values (NrRasterArgs.halo); False makes the
+# backward re-shade its halos instead (same results; the parity tests cover both)
+_HALO_CACHE = os.environ.get("NR_HALO_CACHE", "1") != "0"
+
+
 class Rasterize(torch.autograd.Function):
     """rasterize_core (rasterize.py:194-329) as one Function: vertices [B,V,3] (+ textures) ->
     images [B, C, s, s]; backward returns d/dvertices and d/dtextures."""
@@ -217,20 +226,26 @@ class Rasterize(torch.autograd.Function):
         S = cfg.image_size * (2 if cfg.aa else 1)
         L = _lib.lib()
         fim = torch.empty((B, S, S), dtype=torch.int32, device=dev)
-        face_records = torch.empty((B, cfg.F, 9), dtype=torch.float32, device=dev)
+        face_records = torch.empty((B, cfg.F, 16), dtype=torch.float32, device=dev)  # nr_raster.h NrRasterArgs
         rgb = bool(cfg.flags & _lib.NR_DRAW_RGB)
         face_uv = None
         if rgb:
             uv_items = 1 if vertices_textures.stride(0) == 0 else B
-            face_uv = torch.empty((uv_items, cfg.F, 6), dtype=torch.float32, device=dev)
+            face_uv = torch.empty((uv_items, cfg.F, 8), dtype=torch.float32, device=dev)
         ws = torch.empty(L.nr_workspace_bytes(B, cfg.F, S), dtype=torch.uint8, device=dev)
         images = torch.empty((B, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev)
-        a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws)
+        # tile-border image values for the backward (nr_raster.h NrRasterArgs.halo), only when one will run
+        halo = None
+        if _HALO_CACHE and any(ctx.needs_input_grad[:2]):
+            halo = torch.empty(L.nr_halo_bytes(B, cfg.image_size, int(cfg.aa), cfg.flags) // 4, dtype=torch.float32,
+                               device=dev)
+        a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws,
+                  halo=halo)
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_forward(a, _lib.ptr(images), _lib.stream_of(vertices)), "nr_rasterize_forward")
         ctx.cfg = cfg
         ctx.save_for_backward(vertices, textures, vertices_textures, faces, faces_textures, face_records, face_uv,
-                              fim)
+                              fim, halo)
         ctx.mark_non_differentiable(fim)
         # no zero-filled gradient for the int32 face-index output (a 67 MB fill per backward at the
         # headline size otherwise)
@@ -240,7 +255,7 @@ class Rasterize(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_images, _grad_fim):
         cfg = ctx.cfg
-        vertices, textures, vt, faces, ft, face_records, face_uv, fim = ctx.saved_tensors
+        vertices, textures, vt, faces, ft, face_records, face_uv, fim, halo = ctx.saved_tensors
         if grad_images is None:
             return None, None, None, None, None, None
         grad_images = grad_images.contiguous()
@@ -257,7 +272,7 @@ class Rasterize(torch.autograd.Function):
         H, W = cfg.tex_hw
         ws = torch.empty(L.nr_backward_workspace_bytes(cfg.B, cfg.F, tex_items, H, W), dtype=torch.uint8, device=dev)
         adj = _vertex_adjacency(faces, cfg.V)
-        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj)
+        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo)
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),
                                                ws.numel(), _lib.stream_of(vertices)), "nr_rasterize_backward")

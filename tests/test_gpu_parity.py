@@ -385,3 +385,60 @@ def test_reference_binding_module(golden, dev):
             gin = torch.zeros_like(data)
             assert rc.mask_foreground_backward(fim, gin, data, 3) is gin
             assert torch.equal(gin, torch.where(fg, data, torch.zeros_like(data)))
+
+
+def test_exact_division_shortcut(dev):
+    """div_nr (the compiler's f32 division sequence without v_div_scale / v_div_fixup) equals IEEE
+    a / b bit for bit over the operand range the kernels guard: |a|, |b| in [2^-81, 2^62] and
+    [2^-20, 2^20] respectively, quotients normal, exponent gap < 96 (random mantissas, every
+    exponent pair, and mantissas next to powers of two)."""
+    from neural_renderer_v2_pytorch_amd import _lib
+    g = torch.Generator(device=dev).manual_seed(5)
+    n = 1 << 24
+    ea = torch.randint(-81, 62, (n,), device=dev, generator=g).float()
+    eb = torch.randint(-20, 20, (n,), device=dev, generator=g).float()
+    ma = 1 + torch.rand(n, device=dev, generator=g)
+    mb = 1 + torch.rand(n, device=dev, generator=g)
+    # mantissas at the ends of the binade (all-ones / just above 1)
+    edge = torch.rand(n, device=dev, generator=g) < 0.25
+    ulp = torch.randint(0, 8, (n,), device=dev, generator=g).float() * 2.0 ** -23
+    mb = torch.where(edge, torch.where(torch.rand(n, device=dev, generator=g) < 0.5, 2 - 2.0 ** -23 - ulp, 1 + ulp), mb)
+    sa = torch.where(torch.rand(n, device=dev, generator=g) < 0.5, -1.0, 1.0)
+    sb = torch.where(torch.rand(n, device=dev, generator=g) < 0.5, -1.0, 1.0)
+    a = (sa * ma * torch.exp2(ea)).float().contiguous()
+    b = (sb * mb * torch.exp2(eb)).float().contiguous()
+    qf, qi = torch.empty_like(a), torch.empty_like(a)
+    _lib.check(_lib.lib().nr_selftest_division(_lib.ptr(a), _lib.ptr(b), _lib.ptr(qf), _lib.ptr(qi), n,
+                                               _lib.stream_of(a)), "nr_selftest_division")
+    assert torch.equal(qi, a / b)  # the IEEE leg is torch's division too
+    bad = (qf.view(torch.int32) != qi.view(torch.int32))
+    assert not bad.any(), (int(bad.sum()), a[bad][:4].tolist(), b[bad][:4].tolist())
+
+
+@pytest.mark.parametrize("aa,size", [(True, 64), (False, 70)])
+def test_halo_cache_matches_reshading(dev, aa, size):
+    """The backward's tile halos read from the forward's halo cache give the same gradients as
+    re-shading them (NrRasterArgs.halo NULL); includes a size that is not a multiple of the tiles."""
+    B = 3
+    proj, f = _ico_batch(3, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.rand(tex.shape, generator=torch.Generator().manual_seed(4)).to(dev)
+    g = torch.randn((B, 5, size, size), generator=torch.Generator().manual_seed(6)).to(dev)
+    grads = []
+    for use in (True, False):
+        nrr._HALO_CACHE = use
+        try:
+            pv = proj.to(dev).requires_grad_(True)
+            tx = tex.clone().requires_grad_(True)
+            params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                                       faces_textures=torch.as_tensor(ft, device=dev),
+                                       textures=tx[None].expand(B, -1, -1, -1))
+            img = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params,
+                                     nr.RasterizeHyperparam(image_size=size, anti_aliasing=aa))
+            img.backward(g)
+            grads.append((img.detach(), pv.grad, tx.grad))
+        finally:
+            nrr._HALO_CACHE = True
+    assert torch.equal(grads[0][0], grads[1][0])
+    close_grads(grads[0][1], grads[1][1], "grad vertices")
+    close_grads(grads[0][2], grads[1][2], "grad textures")

@@ -29,6 +29,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <cstdlib>
 #include <string>
 
 #include "nr_raster.h"
@@ -243,12 +244,13 @@ __device__ __forceinline__ float recip_exact(float x) {
 
 struct TexView {
     const float* __restrict__ tex;
-    long long sb, sc, sp;
+    long long sb;   // item stride (uniform 64-bit part)
+    int sc, sp;     // channel / texel strides: one item's view spans < 2^31 elements (validate_raster)
     int H, W;
 };
 
 __device__ __forceinline__ float texel(const TexView& t, int b, int c, int p) {
-    return t.tex[(long long)b * t.sb + (long long)c * t.sc + (long long)p * t.sp];
+    return t.tex[(long long)b * t.sb + (c * t.sc + p * t.sp)];
 }
 
 // sample_textures (rasterize.py:100-153) for one foreground pixel, with the intermediates the
@@ -351,7 +353,7 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
         const bool wfast = face_weights(xp, yp, f, w);
         if (R) {
             TexSample s;
-            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)fi * 8;
+            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + fi * 8;
             sample_texture(f, w, wfast, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s);
             r = s.rgb[0];
             gg = s.rgb[1];
@@ -723,6 +725,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
     const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
     const int2* bbb = bbox + (long long)b * F;
     const float* frb = face_records + (long long)b * F * rs;
+    int32_t* __restrict__ fimb = fim + (long long)b * S * S;
 
     for (int wbase = 0; wbase < g.nwords; wbase += NT) {
         const int w = wbase + t;
@@ -743,7 +746,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
                 const int n = min(FCAP, nc - j0);
                 if (t < n) {
                     const int f = s_cand[j0 + t];
-                    stage_face(s_face[t], frb + (long long)f * rs, f, bbb[f]);
+                    stage_face(s_face[t], frb + f * rs, f, bbb[f]);
                     s_box[t] = s_face[t][0];
                 }
                 __syncthreads();
@@ -772,7 +775,7 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
         const int px = bx0 + lx[k], py = by0 + ly[k];
-        if (px < S && py < S) fim[((long long)b * S + py) * S + px] = best[k];
+        if (px < S && py < S) fimb[py * S + px] = best[k];
     }
 }
 
@@ -845,34 +848,34 @@ __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_re
     if (!aa) {
         // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
         const int y = S - 1 - oi, x = S - 1 - oj;
-        const int fi = fb[(long long)y * S + x];
+        const int fi = fb[y * S + x];
         Face f = empty_face();
-        if (fi >= 0) f = load_face_rec(frb + (long long)fi * FACE_REC);
+        if (fi >= 0) f = load_face_rec(frb + fi * FACE_REC);
         float v[MAXC];
         shade_pixel(sh, b, fi, f, pix_center(x, S), pix_center(y, S), v);
 #pragma unroll
         for (int c = 0; c < MAXC; c++)
-            if (c < sh.C) ob[(long long)c * s * s] = v[c];
+            if (c < sh.C) ob[c * s * s] = v[c];
         if (halo) halo_store(halo, b, sh.C, S, x, y, v);
         return;
     }
     // 2x2 average of the flipped image (rasterize.py:321-328): output (oi, oj) reads internal rows
     // iy, iy+1 and columns ix, ix+1 with a=(iy+1,ix+1) b=(iy,ix+1) c=(iy+1,ix) d=(iy,ix)
     const int iy = S - 2 - 2 * oi, ix = S - 2 - 2 * oj;
-    const int2 f0 = *reinterpret_cast<const int2*>(fb + (long long)iy * S + ix);        // d, b
-    const int2 f1 = *reinterpret_cast<const int2*>(fb + (long long)(iy + 1) * S + ix);  // c, a
+    const int2 f0 = *reinterpret_cast<const int2*>(fb + iy * S + ix);        // d, b
+    const int2 f1 = *reinterpret_cast<const int2*>(fb + (iy + 1) * S + ix);  // c, a
     const int fis[4] = {f1.y, f0.y, f1.x, f0.x};
     const int ys[4] = {iy + 1, iy, iy + 1, iy}, xs[4] = {ix + 1, ix + 1, ix, ix};
     float v[4][MAXC];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         Face f = empty_face();
-        if (fis[q] >= 0) f = load_face_rec(frb + (long long)fis[q] * FACE_REC);
+        if (fis[q] >= 0) f = load_face_rec(frb + fis[q] * FACE_REC);
         shade_pixel(sh, b, fis[q], f, pix_center(xs[q], S), pix_center(ys[q], S), v[q]);
     }
 #pragma unroll
     for (int c = 0; c < MAXC; c++)
-        if (c < sh.C) ob[(long long)c * s * s] = (((v[0][c] + v[1][c]) + v[2][c]) + v[3][c]) / 4.f;
+        if (c < sh.C) ob[c * s * s] = (((v[0][c] + v[1][c]) + v[2][c]) + v[3][c]) / 4.f;
     if (halo) {
         // this thread's 2x2 internal pixels on the backward's tile borders: rows iy (top border) /
         // iy + 1 (bottom border) as float2 pairs, columns ix (left) / ix + 1 (right)
@@ -1053,26 +1056,28 @@ struct BwdArgs {
     int step_pow2;                     // x / step == x * inv_step exactly
 };
 
-__device__ __forceinline__ void upstream_grad(const BwdArgs& a, int C, int b, int y, int x, int S, float* G) {
+// upstream gradient of internal pixel (x, y): the flip / 2x2-mean backward is an index map and /4.
+// gi: this item's [C, s, s] upstream gradient (32-bit offsets inside it)
+__device__ __forceinline__ void upstream_grad(const BwdArgs& a, const float* __restrict__ gi, int C, int y, int x, int S,
+                                              float* G) {
     if (a.aa) {
         const int s = a.s;
-        const int oi = (S - 1 - y) >> 1, oj = (S - 1 - x) >> 1;
+        const int o = ((S - 1 - y) >> 1) * s + ((S - 1 - x) >> 1);
 #pragma unroll
-        for (int c = 0; c < MAXC; c++)
-            G[c] = c < C ? a.grad_images[(((long long)b * C + c) * s + oi) * s + oj] / 4.f : 0.f;
+        for (int c = 0; c < MAXC; c++) G[c] = c < C ? gi[c * s * s + o] / 4.f : 0.f;
     } else {
+        const int o = (S - 1 - y) * S + (S - 1 - x);
 #pragma unroll
-        for (int c = 0; c < MAXC; c++)
-            G[c] = c < C ? a.grad_images[(((long long)b * C + c) * S + (S - 1 - y)) * S + (S - 1 - x)] : 0.f;
+        for (int c = 0; c < MAXC; c++) G[c] = c < C ? gi[c * S * S + o] : 0.f;
     }
 }
 
-__device__ __forceinline__ float upstream_one(const BwdArgs& a, int C, int b, int y, int x, int S, int c) {
+__device__ __forceinline__ float upstream_one(const BwdArgs& a, const float* __restrict__ gi, int y, int x, int S, int c) {
     if (a.aa) {
         const int s = a.s;
-        return a.grad_images[(((long long)b * C + c) * s + ((S - 1 - y) >> 1)) * s + ((S - 1 - x) >> 1)] / 4.f;
+        return gi[c * s * s + ((S - 1 - y) >> 1) * s + ((S - 1 - x) >> 1)] / 4.f;
     }
-    return a.grad_images[(((long long)b * C + c) * S + (S - 1 - y)) * S + (S - 1 - x)];
+    return gi[c * S * S + (S - 1 - y) * S + (S - 1 - x)];
 }
 
 __device__ __forceinline__ float div_step(const BwdArgs& a, float x) { return a.step_pow2 ? x * a.inv_step : x / a.step; }
@@ -1125,6 +1130,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     const int bt = sh.tv.sb ? b : 0;
+    // per-item bases (uniform, 64-bit); per-pixel offsets below are 32-bit
+    const int32_t* __restrict__ fimb = a.fim + (long long)b * S * S;
+    const float* __restrict__ gimb = a.grad_images + (long long)b * C * (a.aa ? a.s * a.s : S * S);
+    const float* __restrict__ frb = a.face_records + (long long)b * a.F * FACE_REC;
+    const float* __restrict__ fuvb = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0);
+    float* __restrict__ gFb = a.grad_faces + (long long)b * a.F * 9;
+    float* __restrict__ g4b = a.grad_tex4 ? a.grad_tex4 + (long long)bt * a.HWp * 4 : nullptr;
     // wave wid owns the 16x8 block at (16 (wid & 1), 8 (wid >> 1)); lane -> column lane & 15, rows lane >> 4 (+4)
     const int lx = (wid & 1) * 16 + (lane & 15);
     const int ly0 = (wid >> 1) * 8 + (lane >> 4);
@@ -1143,8 +1155,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             const bool h_in = t < NHALO && hpy >= 0 && hpy < S && hpx >= 0 && hpx < S;
             int hoff = 0, hcs = 0;
             if (h_in) halo_locate(C, S, hpx, hpy, hoff, hcs);
-            const float* hsrc = a.halo + b * halo_item_floats(S, C) + hoff;
-            const float* gsrc = a.grad_images + (long long)b * C * (a.aa ? a.s * a.s : S * S);
+            // opaque copies of the base pointers: keeps the compiler from sharing these address
+            // computations with step 1's (which would stretch their live ranges over it)
+            const float* hbase = a.halo;
+            const float* gbase = a.grad_images;
+            asm volatile("" : "+s"(hbase), "+s"(gbase));
+            const float* hsrc = hbase + b * halo_item_floats(S, C) + hoff;
+            const float* gsrc = gbase + (long long)b * C * (a.aa ? a.s * a.s : S * S);
             if (h_in) gsrc += a.aa ? ((S - 1 - hpy) >> 1) * a.s + ((S - 1 - hpx) >> 1) : (S - 1 - hpy) * S + (S - 1 - hpx);
             const int gplane = a.aa ? a.s * a.s : S * S;
 #pragma unroll
@@ -1152,7 +1169,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                 if (c < C) {
                     __builtin_amdgcn_global_load_lds((const void*)(hsrc + c * hcs),
                                                      (void __attribute__((address_space(3)))*)(&s_hI[c][wid * 64]), 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((const void*)(gsrc + (long long)c * gplane),
+                    __builtin_amdgcn_global_load_lds((const void*)(gsrc + c * gplane),
                                                      (void __attribute__((address_space(3)))*)(&s_hG[c][wid * 64]), 4, 0, 0);
                 }
             }
@@ -1170,7 +1187,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         const int py = ty0 + ly0 + 4 * k;
         const bool inside = px < S && py < S;
         BwdPix& q = P[k];
-        q.fi = inside ? a.fim[((long long)b * S + py) * S + px] : -1;
+        q.fi = inside ? fimb[py * S + px] : -1;
         q.pos = -1;
         q.wx = q.wy = INT_MIN;
         q.w[0] = q.w[1] = q.w[2] = 0.f;
@@ -1179,7 +1196,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         q.ay = q.by = q.ax = q.bx = 0.f;
 #pragma unroll
         for (int c = 0; c < MAXC; c++) I2[k][c] = G2[k][c] = 0.f;
-        if (inside) upstream_grad(a, C, b, py, px, S, G2[k]);
+        if (inside) upstream_grad(a, gimb, C, py, px, S, G2[k]);
     }
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -1188,7 +1205,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         if (q.fi < 0) continue;
         const float yp = pix_center(py, S);
         const float* G = G2[k];
-        Face f = load_face_rec(a.face_records + ((long long)b * a.F + q.fi) * FACE_REC);
+        Face f = load_face_rec(frb + q.fi * FACE_REC);
 #ifndef NR_BWD_FASTDIV
         f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
 #endif
@@ -1197,7 +1214,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
         if (rgb) {
             TexSample s;
-            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + (long long)q.fi * 8;
+            const float* fuv = fuvb + q.fi * 8;
             sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s);
             r = s.rgb[0];
             gg = s.rgb[1];
@@ -1246,7 +1263,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                     // outside the face window: direct atomics (texel index as sampled)
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        float* gtg = a.grad_tex4 + ((long long)bt * a.HWp + s.idx[i]) * 4;
+                        float* gtg = g4b + s.idx[i] * 4;
 #pragma unroll
                         for (int ch = 0; ch < 3; ch++) {
                             const float v = G[ch] * s.wt[i];
@@ -1292,7 +1309,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             dep = depth_value(f, w, wfast);
             // depth channel gradient reloaded (cache hit) rather than a runtime-indexed register array
             const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
-            const float gd = upstream_one(a, C, b, py, px, S, dc);
+            const float gd = upstream_one(a, gimb, py, px, S, dc);
             const float g_s = -gd * (dep * dep);
             const float z[3] = {f.z0, f.z1, f.z2};
 #pragma unroll
@@ -1346,11 +1363,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 #pragma unroll
         for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
         if (!(NR_ABLATE & 16) && h_in) {
-            const int hf = a.fim[((long long)b * S + hpy) * S + hpx];
+            const int hf = fimb[hpy * S + hpx];
             Face ff = empty_face();
-            if (hf >= 0) ff = load_face_rec(a.face_records + ((long long)b * a.F + hf) * FACE_REC);
+            if (hf >= 0) ff = load_face_rec(frb + hf * FACE_REC);
             shade_pixel(sh, b, hf, ff, pix_center(hpx, S), pix_center(hpy, S), hI);
-            upstream_grad(a, C, b, hpy, hpx, S, hG);
+            upstream_grad(a, gimb, C, hpy, hpx, S, hG);
         }
         const int hl = hy * HW_ + hx;
 #pragma unroll
@@ -1474,9 +1491,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         } else if (chunk < 3) {
             const int x = wx + tdx, y = wy + tdy;
             if (want_tex && v != 0.f && wx != INT_MIN && x < sh.tv.W && y < sh.tv.H)
-                unsafeAtomicAdd(a.grad_tex4 + ((long long)bt * a.HWp + (long long)y * sh.tv.W + x) * 4 + chunk, v);
+                unsafeAtomicAdd(g4b + (y * sh.tv.W + x) * 4 + chunk, v);
         } else if (tt < 9) {
-            if (v != 0.f) unsafeAtomicAdd(a.grad_faces + ((long long)b * a.F + key) * 9 + tt, v);
+            if (v != 0.f) unsafeAtomicAdd(gFb + key * 9 + tt, v);
         }
     }
 }
@@ -1528,6 +1545,9 @@ int validate_raster(const NrRasterArgs* a, bool need_workspace) {
         if (!a->vertices_textures || !a->faces_textures || !a->textures || !a->face_uv)
             return fail(NR_ERR_ARGS, "rgb requested without textures");
         if (a->tex_height <= 0 || a->tex_width <= 0) return fail(NR_ERR_ARGS, "bad texture size");
+        const long long span = 2 * std::llabs(a->tex_stride_c) +
+                               ((long long)a->tex_height * a->tex_width - 1) * std::llabs(a->tex_stride_p) + 1;
+        if (span >= (1ll << 31)) return fail(NR_ERR_ARGS, "texture item spans 2^31 elements or more");
     }
     const Geom g = make_geom(a->num_faces, S);
     const size_t need = ws_bbox_bytes(a->batch_size, a->num_faces) + ws_mask_bytes(a->batch_size, g);
@@ -1543,8 +1563,8 @@ Shade make_shade(const NrRasterArgs* a) {
     sh.eps = a->eps;
     sh.tv.tex = a->textures;
     sh.tv.sb = a->tex_stride_b;
-    sh.tv.sc = a->tex_stride_c;
-    sh.tv.sp = a->tex_stride_p;
+    sh.tv.sc = (int)a->tex_stride_c;
+    sh.tv.sp = (int)a->tex_stride_p;
     sh.tv.H = a->tex_height;
     sh.tv.W = a->tex_width;
     sh.face_uv = a->face_uv;

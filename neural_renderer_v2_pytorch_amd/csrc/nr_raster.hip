@@ -1103,6 +1103,19 @@ __device__ __forceinline__ void halo_pixel(int t, int& hy, int& hx) {
     else { hy = 1 + (t - 2 * HW_ - BH); hx = HW_ - 1; }
 }
 
+// Values (v0, v1, v2, v3) held by every lane; lane l ends with v_c summed over the four lanes
+// l & 15 + 16 k, where c = l >> 4.  v_permlane32_swap(A, B) leaves [A_lo | B_lo] and [A_hi | B_hi]
+// (32-lane halves), so their sum is A summed over the halves in the low half and B in the high
+// half; v_permlane16_swap does the same for 16-lane rows.
+__device__ __forceinline__ float chunk_reduce_scatter(float v0, float v1, float v2, float v3) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v2), false, false);
+    const float b0 = __uint_as_float(p[0]) + __uint_as_float(p[1]);  // rows 0,1: v0; rows 2,3: v2
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v1), __float_as_uint(v3), false, false);
+    const float b1 = __uint_as_float(q[0]) + __uint_as_float(q[1]);  // rows 0,1: v1; rows 2,3: v3
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(b0), __float_as_uint(b1), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);           // row c: v_c
+}
+
 // per interior pixel state carried across the stencil's barrier
 struct BwdPix {
     int fi;            // face index (-1: background or outside)
@@ -1475,17 +1488,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                 }
             }
         }
-        // add the 4 member chunks (lanes t, t+16, t+32, t+48)
-        a0 += __shfl_xor(a0, 16, 64);
-        a1 += __shfl_xor(a1, 16, 64);
-        a2 += __shfl_xor(a2, 16, 64);
-        af += __shfl_xor(af, 16, 64);
-        a0 += __shfl_xor(a0, 32, 64);
-        a1 += __shfl_xor(a1, 32, 64);
-        a2 += __shfl_xor(a2, 32, 64);
-        af += __shfl_xor(af, 32, 64);
+        // reduce-scatter over the 4 member chunks (lanes t, t+16, t+32, t+48) with the gfx950 lane
+        // swaps (VALU, no LDS round trip): lane (t, c) ends with the chunk total of value c
+        const float v = chunk_reduce_scatter(a0, a1, a2, af);
         // ---- 4. flush this face: lane (t, c) writes channel c of texel t (c < 3) or face float t (c == 3)
-        const float v = chunk == 0 ? a0 : (chunk == 1 ? a1 : (chunk == 2 ? a2 : af));
         if (NR_ABLATE & 4) {
             asm volatile("" ::"v"(v));
         } else if (chunk < 3) {

@@ -43,6 +43,7 @@ constexpr int TH = 8;              // tile height
 constexpr int NT = TW * TH;        // threads per raster block, one pixel each
 constexpr int COARSE = 32;         // coarse bin edge (pixels) = forward block region; = TW, multiple of TH
 constexpr int SETUP_FACES = 128;   // faces per setup block (4 bitmask words)
+constexpr int SETUP_LDS_WORDS = 4096;  // bin-mask words built in LDS (up to 1024 bins, S <= 1024)
 constexpr int MAXC = 5;            // max output channels
 
 thread_local std::string g_err;
@@ -464,6 +465,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
                                                     int uv_items) {
     __shared__ int2 s_bb[SETUP_FACES];
+    __shared__ uint32_t s_mask[SETUP_LDS_WORDS];
     const int b = blockIdx.y;
     const int f0 = blockIdx.x * SETUP_FACES;
     const int t = threadIdx.x;
@@ -540,9 +542,31 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         s_bb[t] = bb;
     }
     __syncthreads();
-    // coarse-bin bitmask words of this face group: (bin, word) pairs
+    // coarse-bin bitmask words of this face group
     const int w0 = blockIdx.x * (SETUP_FACES / 32);
     const int nw = min(SETUP_FACES / 32, nwords - w0);
+    if (nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS) {
+        // each face sets its bit in the (few) bins its pixel range touches (LDS ds_or), then the
+        // block writes its words out
+        for (int i = t; i < nbins * (SETUP_FACES / 32); i += blockDim.x) s_mask[i] = 0u;
+        __syncthreads();
+        if (t < SETUP_FACES) {
+            const int2 bb = s_bb[t];
+            const int x0 = range_lo(bb.x), x1 = range_hi(bb.x), y0 = range_lo(bb.y), y1 = range_hi(bb.y);
+            if (x0 <= x1 && y0 <= y1) {
+                const int nby = nbins / nbx;
+                for (int by = y0 / COARSE; by <= min(y1 / COARSE, nby - 1); by++)
+                    for (int bx = x0 / COARSE; bx <= min(x1 / COARSE, nbx - 1); bx++)
+                        atomicOr(&s_mask[(by * nbx + bx) * (SETUP_FACES / 32) + (t >> 5)], 1u << (t & 31));
+            }
+        }
+        __syncthreads();
+        for (int p = t; p < nbins * nw; p += blockDim.x) {
+            const int bin = p / nw, wi = p % nw;
+            mask[((long long)b * nbins + bin) * nwords + w0 + wi] = s_mask[bin * (SETUP_FACES / 32) + wi];
+        }
+        return;
+    }
     for (int p = t; p < nbins * nw; p += blockDim.x) {
         const int bin = p / nw, wi = p % nw;
         const int bx0 = (bin % nbx) * COARSE, by0 = (bin / nbx) * COARSE;

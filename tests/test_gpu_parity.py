@@ -267,10 +267,11 @@ def _ico_batch(level, B, dev):
     return proj, f
 
 
-@pytest.mark.parametrize("S,level,B", [(512, 4, 2), (1000, 3, 1), (130, 4, 3)])
+@pytest.mark.parametrize("S,level,B", [(512, 4, 2), (1000, 3, 1), (130, 4, 3), (1100, 2, 1)])
 def test_face_index_large_vs_oracle(oracle_mod, dev, S, level, B):
     """Headline-size face-index map (ico-sphere 5120 faces, 512^2 internal) bit-exact against the
-    brute-force CPU oracle; plus a non-multiple-of-tile size."""
+    brute-force CPU oracle; plus a non-multiple-of-tile size and a size past the LDS bin-mask path
+    of k_face_setup (S > 1024)."""
     proj, f = _ico_batch(level, B, dev)
     fg = proj[:, torch.as_tensor(f).long()].contiguous()
     fim = nrr.compute_face_index_map(fg.to(dev), nr.RasterizeHyperparam(image_size=S))

@@ -272,8 +272,11 @@ struct TexSample {
 
 // uv: the face's 8-float texture record (u0 v0 u1 v1 u2 v2, flag, -); flag 1 = every u, v in
 // {0} u [2^-16, 2^20].  wfast: face_weights took its exact-division path.
+// G (optional, backward): upstream gradient of the rgb channels; then gw[i] = sum_c G[c] T_i[c] for
+// the 4 bilinear texels, from the texel values loaded here (no second load)
 __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], bool wfast, const float* __restrict__ uv,
-                                               const TexView& tv, int bt, float eps, TexSample& s) {
+                                               const TexView& tv, int bt, float eps, TexSample& s,
+                                               const float* G = nullptr, float* gw = nullptr) {
     const float4 uva = reinterpret_cast<const float4*>(uv)[0], uvb = reinterpret_cast<const float4*>(uv)[1];
     const float uvs[6] = {uva.x, uva.y, uva.z, uva.w, uvb.x, uvb.y};
     const bool fast = wfast && (f.flags & FACE_FAST_ZQ) && __float_as_int(uvb.z) != 0;
@@ -318,11 +321,28 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
     s.wt[1] = (s.y1 - s.y) * (s.x - s.x0);
     s.wt[2] = (s.y - s.y0) * (s.x1 - s.x);
     s.wt[3] = (s.y - s.y0) * (s.x - s.x0);
+    const float* tb = tv.tex + (long long)bt * tv.sb;
+    int off[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) off[i] = s.idx[i] * tv.sp;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-        const float t0 = texel(tv, bt, c, s.idx[0]), t1 = texel(tv, bt, c, s.idx[1]);
-        const float t2 = texel(tv, bt, c, s.idx[2]), t3 = texel(tv, bt, c, s.idx[3]);
+        const float* tc = tb + c * tv.sc;
+        const float t0 = tc[off[0]], t1 = tc[off[1]], t2 = tc[off[2]], t3 = tc[off[3]];
         s.rgb[c] = ((s.wt[0] * t0 + s.wt[1] * t1) + s.wt[2] * t2) + s.wt[3] * t3;
+        if (G) {
+            if (c == 0) {
+                gw[0] = G[0] * t0;
+                gw[1] = G[0] * t1;
+                gw[2] = G[0] * t2;
+                gw[3] = G[0] * t3;
+            } else {
+                gw[0] = gw[0] + G[c] * t0;
+                gw[1] = gw[1] + G[c] * t1;
+                gw[2] = gw[2] + G[c] * t2;
+                gw[3] = gw[3] + G[c] * t3;
+            }
+        }
     }
 }
 
@@ -1252,22 +1272,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         if (rgb) {
             TexSample s;
             const float* fuv = fuvb + q.fi * 8;
-            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s);
+            // bilinear: images = sum_i wt_i T_i -> textures (staged below) and weights (gw)
+            float gw[4];
+            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s, G, gw);
             r = s.rgb[0];
             gg = s.rgb[1];
             bb = s.rgb[2];
-            // bilinear: images = sum_i wt_i T_i -> textures (staged below) and weights
-            float gw[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                float acc = 0.f;
-#pragma unroll
-                for (int ch = 0; ch < 3; ch++) {
-                    const float tv = texel(sh.tv, bt, ch, s.idx[i]);
-                    acc = (ch == 0) ? G[ch] * tv : acc + G[ch] * tv;
-                }
-                gw[i] = acc;
-            }
             q.ay = s.y1 - s.y;
             q.by = s.y - s.y0;
             q.ax = s.x1 - s.x;

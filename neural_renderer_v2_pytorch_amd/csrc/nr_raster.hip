@@ -657,6 +657,11 @@ __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, f
     best += (int)e[0].x;  // timing build: no per-pixel test
     return;
 #endif
+    // The rejections of .cu:94-126 are independent of each other (none changes the state), so their
+    // order is free: the depth-bound reject .cu:124-126 goes first, as it is the cheapest and lets a
+    // whole wave skip a face hidden behind what its pixels already hold.
+    const float4 q1 = e[1];
+    if (depth_min < q1.z) return;
     const float4 q0 = e[0];
     // .cu:94-97 (min/max form, exact for non-NaN faces)
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
@@ -668,9 +673,6 @@ __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, f
     if (c1 * c2 < 0) return;
     const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
     if (c2 * c3 < 0) return;
-    const float4 q1 = e[1];
-    // .cu:124-126
-    if (depth_min < q1.z) return;
 #if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 2
     best = __float_as_int(q1.w);  // timing build: no division block
     return;

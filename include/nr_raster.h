@@ -53,6 +53,8 @@ enum { NR_DRAW_RGB = 1, NR_DRAW_SILHOUETTES = 2, NR_DRAW_DEPTH = 4 };
 
 NR_API const char* nr_last_error(void);
 NR_API int nr_version(void);
+/* sizeof(NrRasterArgs), for bindings to check their mirror of the struct */
+NR_API size_t nr_raster_args_size(void);
 
 /* Scratch bytes needed by the face-index map for B items, F faces, S x S internal pixels
  * (per-face screen bounding boxes + coarse-bin face bitmasks). */
@@ -119,7 +121,26 @@ typedef struct NrRasterArgs {
      * values of the backward's tile borders there and the backward reads them instead of shading
      * its tile halos again; NULL = backward re-shades (same results). */
     float* halo;
+    /* lights (rasterize.py:252-283, lights.py:4-39), only with NR_DRAW_RGB.  lights holds
+     * [num_lights][B][NR_LIGHT_FLOATS] records in list order: kind (NR_LIGHT_*), backside, colour
+     * r g b, then direction x y z (directional) or alpha (specular, slot 5).  The smooth normal
+     * map (rasterize.py:162-190) needs: */
+    int num_lights;
+    const float* lights;
+    float* face_normals;             /* [B, F, 3] scratch (forward) */
+    float* vertex_normals;           /* [B, V, 4]: normalised normal + norm; written by the forward,
+                                        read by the backward */
+    const int32_t* normal_offsets;   /* [V + 1] CSR vertex -> its distinct faces (the reference's */
+    const int32_t* normal_faces;     /*          one-hot [F, V] matrix, rasterize.py:173-179)     */
+    /* backgrounds, only with NR_DRAW_RGB: [B, 3, S, S] at the internal size (x stride 1); the rgb of
+     * background pixels is backgrounds[b, c, S-1-y, S-1-x] (the blend of
+     * neural_renderer_chainer/rasterize.py:574-577; the torch blend_backgrounds raises) */
+    const float* backgrounds;
+    long long bg_stride_b, bg_stride_c, bg_stride_y;
+    float* grad_backgrounds;         /* backward output [B, 3, S, S] contiguous, fully written; or NULL */
 } NrRasterArgs;
+
+enum { NR_LIGHT_AMBIENT = 0, NR_LIGHT_DIRECTIONAL = 1, NR_LIGHT_SPECULAR = 2, NR_LIGHT_FLOATS = 8 };
 
 /* Channels in output order: rgb (3), silhouettes (1), depth (1) -- those enabled by draw_flags. */
 NR_API int nr_num_channels(int draw_flags);
@@ -130,10 +151,11 @@ NR_API int nr_rasterize_forward(const NrRasterArgs* args, float* images, void* s
 /* Bytes of NrRasterArgs.halo for B items at output size s (internal 2s with anti-aliasing). */
 NR_API size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw_flags);
 
-/* Scratch bytes of nr_rasterize_backward: per-face gradient records [B, F, 9] and the texture
- * gradient accumulator [texture_items, H*W rounded up to 4, 4]. */
-NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int texture_items, int tex_height,
-                                          int tex_width);
+/* Scratch bytes of nr_rasterize_backward: per-face gradient records [B, F, 9], the texture
+ * gradient accumulator [texture_items, H*W rounded up to 4, 4], and with lights the per-face
+ * vertex-normal gradients [B, F, 9] and per-vertex normal gradients [B, V, 3]. */
+NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num_vertices, int texture_items,
+                                          int tex_height, int tex_width, int num_lights);
 
 /* Backward of nr_rasterize_forward for upstream grad_images [B, C, s, s] (contiguous), given the
  * state the forward saved in `args`.  Writes grad_vertices [B, V, 3] and, with NR_DRAW_RGB and

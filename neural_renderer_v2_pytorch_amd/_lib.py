@@ -23,7 +23,7 @@ EXPORTS = [
     "nr_compute_weight_map", "nr_mask_foreground_forward", "nr_mask_foreground_backward",
     "nr_differentiation_backward", "nr_num_channels", "nr_rasterize_forward", "nr_rasterize_backward",
     "nr_backward_workspace_bytes", "nr_profile_enable", "nr_profile_read",
-    "nr_selftest_division", "nr_halo_bytes",
+    "nr_selftest_division", "nr_halo_bytes", "nr_raster_args_size",
 ]
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
@@ -42,7 +42,13 @@ class NrRasterArgs(ctypes.Structure):
         ("face_records", c_void_p), ("face_uv", c_void_p), ("face_index", c_void_p),
         ("workspace", c_void_p), ("workspace_bytes", c_size_t),
         ("vertex_offsets", c_void_p), ("vertex_faces", c_void_p), ("halo", c_void_p),
+        ("num_lights", c_int), ("lights", c_void_p), ("face_normals", c_void_p), ("vertex_normals", c_void_p),
+        ("normal_offsets", c_void_p), ("normal_faces", c_void_p),
+        ("backgrounds", c_void_p), ("bg_stride_b", c_ll), ("bg_stride_c", c_ll), ("bg_stride_y", c_ll),
+        ("grad_backgrounds", c_void_p),
     ]
+
+NR_LIGHT_AMBIENT, NR_LIGHT_DIRECTIONAL, NR_LIGHT_SPECULAR, NR_LIGHT_FLOATS = 0, 1, 2, 8
 
 
 _lib = None
@@ -73,7 +79,9 @@ def lib():
     L.nr_rasterize_backward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_size_t, c_void_p]
     L.nr_backward_workspace_bytes.restype = c_size_t
-    L.nr_backward_workspace_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int]
+    L.nr_backward_workspace_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int]
+    L.nr_raster_args_size.restype = c_size_t
+    L.nr_raster_args_size.argtypes = []
     L.nr_halo_bytes.restype = c_size_t
     L.nr_halo_bytes.argtypes = [c_int, c_int, c_int, c_int]
     L.nr_selftest_division.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_void_p]
@@ -81,7 +89,7 @@ def lib():
     L.nr_profile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(c_float)]
     for name in EXPORTS:
         if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels", "nr_backward_workspace_bytes",
-                        "nr_halo_bytes"):
+                        "nr_halo_bytes", "nr_raster_args_size"):
             getattr(L, name).restype = c_int
     _lib = L
     return L

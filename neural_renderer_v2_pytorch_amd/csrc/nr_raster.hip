@@ -361,13 +361,88 @@ struct Shade {
     TexView tv;
     const float* __restrict__ face_uv;
     long long uv_bstride;  // F*8 or 0
+    // lights (rgb only): records [nl][B][NR_LIGHT_FLOATS], vertex normals [B, V, 4], face corners
+    int nl, B, V;
+    const float* __restrict__ lights;
+    const float* __restrict__ vnorm;
+    const int32_t* __restrict__ fidx;
+    // backgrounds (rgb only): [B, 3, S, S], x stride 1
+    const float* __restrict__ bg;
+    long long bg_sb;
+    int bg_sc, bg_sy;
 };
+
+// torch.relu (NaN stays NaN)
+__device__ __forceinline__ float t_relu(float x) { return x > 0.f ? x : (x != x ? x : 0.f); }
+
+// smooth normal map at a pixel of face fi (rasterize.py:185-187): sum_k w_k n_k over the face's
+// corner vertex normals, per component ((w0 n0 + w1 n1) + w2 n2)
+__device__ __forceinline__ void pixel_normal(const Shade& sh, int b, int fi, const float w[3], float n[3]) {
+    const float* vb = sh.vnorm + (long long)b * sh.V * 4;
+    float c[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float4 v = *reinterpret_cast<const float4*>(vb + sh.fidx[fi * 3 + k] * 4);
+        c[k][0] = v.x;
+        c[k][1] = v.y;
+        c[k][2] = v.z;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) n[j] = (w[0] * c[0][j] + w[1] * c[1][j]) + w[2] * c[2][j];
+}
+
+// the light loop of rasterize.py:252-281 for one pixel: colour weights cw (starting from 0, lights
+// added in list order); with gcw != nullptr, instead accumulate dL/dn into gn given dL/dcw = gcw
+__device__ __forceinline__ void light_weights(const Shade& sh, int b, const float n[3], float cw[3],
+                                              const float* gcw = nullptr, float* gn = nullptr) {
+    cw[0] = cw[1] = cw[2] = 0.f;
+    for (int l = 0; l < sh.nl; l++) {
+        const float* L = sh.lights + ((long long)l * sh.B + b) * NR_LIGHT_FLOATS;
+        const int kind = (int)L[0];
+        const bool back = L[1] != 0.f;
+        const float col[3] = {L[2], L[3], L[4]};
+        if (kind == NR_LIGHT_AMBIENT) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) cw[c] = cw[c] + col[c];
+            continue;
+        }
+        // intensity = sum(-d * n) with d the light direction, or (0, 0, 1) for specular
+        const float d0 = kind == NR_LIGHT_DIRECTIONAL ? L[5] : 0.f;
+        const float d1 = kind == NR_LIGHT_DIRECTIONAL ? L[6] : 0.f;
+        const float d2 = kind == NR_LIGHT_DIRECTIONAL ? L[7] : 1.f;
+        const float raw = ((-d0) * n[0] + (-d1) * n[1]) + (-d2) * n[2];
+        float s = back ? fabsf(raw) : t_relu(raw);
+        const float alpha = L[5];
+        float ds = back ? (raw > 0.f ? 1.f : (raw < 0.f ? -1.f : 0.f)) : (raw > 0.f ? 1.f : 0.f);  // d s / d raw
+        if (kind == NR_LIGHT_SPECULAR) {
+            const float p = powf(s, alpha);
+            ds = ds * (alpha * powf(s, alpha - 1.f));  // torch pow backward: exponent * base^(exponent - 1)
+            s = p;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) cw[c] = cw[c] + s * col[c];
+        if (gn) {
+            const float gs = ((gcw[0] * col[0] + gcw[1] * col[1]) + gcw[2] * col[2]) * ds;
+            gn[0] += gs * (-d0);
+            gn[1] += gs * (-d1);
+            gn[2] += gs * (-d2);
+        }
+    }
+}
+
+// background colour of internal pixel (x, y): backgrounds[b, c, S-1-y, S-1-x]
+__device__ __forceinline__ void background(const Shade& sh, int b, int x, int y, int S, float bgc[3]) {
+    const float* p = sh.bg + (long long)b * sh.bg_sb + (S - 1 - y) * sh.bg_sy + (S - 1 - x);
+#pragma unroll
+    for (int c = 0; c < 3; c++) bgc[c] = p[c * sh.bg_sc];
+}
 
 // All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth), written
 // to compile-time slots of out[MAXC] (runtime-indexed register arrays would spill to scratch).
-__device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, float xp, float yp,
+__device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, int x, int y, int S,
                                             float* out) {
     const bool R = (sh.draw & NR_DRAW_RGB) != 0, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
+    const float xp = pix_center(x, S), yp = pix_center(y, S);
     float r = 0.f, gg = 0.f, bb = 0.f, sil = 0.f, dep = 0.f;
     if (fi >= 0) {
         float w[3];
@@ -379,9 +454,25 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
             r = s.rgb[0];
             gg = s.rgb[1];
             bb = s.rgb[2];
+            if (sh.nl) {  // rgb_map *= color_weight_map (rasterize.py:283)
+                float n[3], cw[3];
+                pixel_normal(sh, b, fi, w, n);
+                light_weights(sh, b, n, cw);
+                r = r * cw[0];
+                gg = gg * cw[1];
+                bb = bb * cw[2];
+            }
         }
         sil = 1.f;
         if (sh.draw & NR_DRAW_DEPTH) dep = depth_value(f, w, wfast);
+    }
+    if (R && sh.bg) {  // fg * rgb + (1 - fg) * bg (chainer rasterize.py:576)
+        float bgc[3];
+        background(sh, b, x, y, S, bgc);
+        const float fg = fi >= 0 ? 1.f : 0.f;
+        r = fg * r + (1.f - fg) * bgc[0];
+        gg = fg * gg + (1.f - fg) * bgc[1];
+        bb = fg * bb + (1.f - fg) * bgc[2];
     }
     out[0] = R ? r : (Sl ? sil : dep);
     out[1] = R ? gg : dep;
@@ -483,7 +574,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     uint32_t* __restrict__ mask, int nbx, int nbins, int nwords,
                                                     const float* __restrict__ vt, long long vt_bstride, int Vt,
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
-                                                    int uv_items) {
+                                                    int uv_items, float* __restrict__ fnorm) {
     __shared__ int2 s_bb[SETUP_FACES];
     __shared__ uint32_t s_mask[SETUP_LDS_WORDS];
     const int b = blockIdx.y;
@@ -521,6 +612,15 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                 rec[2] = make_float4(c[8], rcp_nr(c[2]), rcp_nr(c[5]), rcp_nr(c[8]));
                 rec[3] = make_float4(rcp_nr(c[2] + 1e-10f), rcp_nr(c[5] + 1e-10f), rcp_nr(c[8] + 1e-10f),
                                      __int_as_float(flags));
+                if (fnorm) {
+                    // face normal cross(v1 - v0, v2 - v1) (rasterize.py:166-170; torch.cross component order)
+                    const float a0 = c[3] - c[0], a1 = c[4] - c[1], a2 = c[5] - c[2];
+                    const float b0 = c[6] - c[3], b1 = c[7] - c[4], b2 = c[8] - c[5];
+                    float* nf = fnorm + ((long long)b * F + f) * 3;
+                    nf[0] = a1 * b2 - a2 * b1;
+                    nf[1] = a2 * b0 - a0 * b2;
+                    nf[2] = a0 * b1 - a1 * b0;
+                }
             } else {
                 const float* rec = face_records + ((long long)b * F + f) * 9;  // caller's [B, F, 3, 3]
 #pragma unroll
@@ -601,6 +701,27 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         }
         mask[((long long)b * nbins + bin) * nwords + w0 + wi] = bits;
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// vertex normals (rasterize.py:171-182): u = sum of the normals of the vertex's distinct faces (the
+// reference's one-hot [F, V] matmul), n = u / max(|u|, 1e-12) (F.normalize); stored as (n, |u|)
+__global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t* __restrict__ off,
+                                 const int32_t* __restrict__ vfaces, float* __restrict__ vnorm, int F, int V, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / V), v = (int)(i % V);
+    const float* fb = fnorm + (long long)b * F * 3;
+    float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+    for (int e = off[v]; e < off[v + 1]; e++) {
+        const float* nf = fb + vfaces[e] * 3;
+        u0 += nf[0];
+        u1 += nf[1];
+        u2 += nf[2];
+    }
+    const float len = sqrtf((u0 * u0 + u1 * u1) + u2 * u2);
+    const float d = fmaxf(len, 1e-12f);
+    reinterpret_cast<float4*>(vnorm)[i] = make_float4(u0 / d, u1 / d, u2 / d, len);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -878,9 +999,13 @@ __device__ __forceinline__ void halo_store(float* __restrict__ halo, int b, int 
 // internal pixels it covers, merged in rgb/sil/depth order, flipped, and 2x2-averaged with the
 // reference's summation order.  Kept out of the rasteriser so that kernel stays lean (registers,
 // occupancy); costs one extra read of the face-index map.
+template <int FEAT>  // 1 = lights, 2 = backgrounds, as k_raster_bwd
 __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
-                                               int F, int S, Shade sh, int aa, float* __restrict__ images,
+                                               int F, int S, Shade sh_in, int aa, float* __restrict__ images,
                                                float* __restrict__ halo) {
+    Shade sh = sh_in;
+    if (!(FEAT & 1)) sh.nl = 0;
+    if (!(FEAT & 2)) sh.bg = nullptr;
     const int s = aa ? S / 2 : S;
     const int b = blockIdx.y;
     int blk = blockIdx.x, unused;
@@ -898,7 +1023,7 @@ __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_re
         Face f = empty_face();
         if (fi >= 0) f = load_face_rec(frb + fi * FACE_REC);
         float v[MAXC];
-        shade_pixel(sh, b, fi, f, pix_center(x, S), pix_center(y, S), v);
+        shade_pixel(sh, b, fi, f, x, y, S, v);
 #pragma unroll
         for (int c = 0; c < MAXC; c++)
             if (c < sh.C) ob[c * s * s] = v[c];
@@ -917,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_re
     for (int q = 0; q < 4; q++) {
         Face f = empty_face();
         if (fis[q] >= 0) f = load_face_rec(frb + fis[q] * FACE_REC);
-        shade_pixel(sh, b, fis[q], f, pix_center(xs[q], S), pix_center(ys[q], S), v[q]);
+        shade_pixel(sh, b, fis[q], f, xs[q], ys[q], S, v[q]);
     }
 #pragma unroll
     for (int c = 0; c < MAXC; c++)
@@ -1074,11 +1199,14 @@ constexpr int BH = 16;                        // block height
 constexpr int HW_ = TW + 2, HH_ = BH + 2, HN = HW_ * HH_;
 constexpr int NHALO = 2 * HW_ + 2 * BH;       // 100 halo pixels
 constexpr int TWIN = 4;                       // texel window edge per face
-constexpr int REC = 20;                       // staged record: ay by ax bx | pos G_rgb[3] | gF[9] | pad
+// staged record: ay by ax bx | pos G_rgb[3] | gF[9] | pad (20 floats); with lights also dL/dnormal[3]
+// and the weights w[3] at 17..22 (24 floats)
+template <bool LIT> constexpr int srec() { return LIT ? 24 : 20; }
 constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
-constexpr int BWD_LDS_REC = 4 * 128 * REC * 4;
 constexpr int BWD_LDS_HALO = 2 * MAXC * 128 * 4;  // halo staging (step 0), after the I / G planes
-constexpr int BWD_LDS = BWD_LDS_IG + BWD_LDS_HALO > BWD_LDS_REC ? BWD_LDS_IG + BWD_LDS_HALO : BWD_LDS_REC;
+template <bool LIT> constexpr int bwd_lds() {
+    return BWD_LDS_IG + BWD_LDS_HALO > 4 * 128 * srec<LIT>() * 4 ? BWD_LDS_IG + BWD_LDS_HALO : 4 * 128 * srec<LIT>() * 4;
+}
 static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 // experiment switch for timing builds (never set in the shipped library):
 //   2 = no gradient accumulation (steps 3 and 4), 4 = no global atomics (step 4),
@@ -1097,6 +1225,8 @@ struct BwdArgs {
     float* __restrict__ grad_faces;   // [B, F, 9]
     float* __restrict__ grad_tex4;    // [Bt, HWp, 4] or null
     const float* __restrict__ halo;   // halo cache written by the forward, or null (re-shade the halo)
+    float* __restrict__ grad_normals; // [B, F, 9] per-face corner vertex-normal gradients (lights)
+    float* __restrict__ grad_bg;      // [B, 3, S, S] or null
     int F, aa, s, HWp;
     float step, inv_step;
     int step_pow2;                     // x / step == x * inv_step exactly
@@ -1171,10 +1301,20 @@ struct BwdPix {
     float ay, by, ax, bx;
     int pos;           // bilinear top-left texel relative to the face window: dx | dy << 8; -1 none
     int wx, wy;        // face window origin (texels); INT_MIN when not windowed
+    float gn[3];       // lights: dL/d(smooth normal)
 };
 
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh) {
-    __shared__ __attribute__((aligned(16))) float s_raw[BWD_LDS / 4];
+// FEAT: 1 = lights, 2 = backgrounds (separate instantiations keep the plain path lean)
+template <int FEAT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
+    constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0;
+    // features this instantiation does not have become compile-time constants (the shared
+    // shade_pixel then carries no light / background code or arguments)
+    Shade sh = sh_in;
+    if (!LIT) sh.nl = 0;
+    if (!BG) sh.bg = nullptr;
+    constexpr int REC = srec<LIT>();
+    __shared__ __attribute__((aligned(16))) float s_raw[bwd_lds<LIT>() / 4];
     float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
     float(*s_G)[HN] = reinterpret_cast<float(*)[HN]>(s_raw + MAXC * HN);
     const int b = blockIdx.y;
@@ -1253,9 +1393,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         q.gz[0] = q.gz[1] = q.gz[2] = 0.f;
         q.grgb[0] = q.grgb[1] = q.grgb[2] = 0.f;
         q.ay = q.by = q.ax = q.bx = 0.f;
+        q.gn[0] = q.gn[1] = q.gn[2] = 0.f;
 #pragma unroll
         for (int c = 0; c < MAXC; c++) I2[k][c] = G2[k][c] = 0.f;
         if (inside) upstream_grad(a, gimb, C, py, px, S, G2[k]);
+        if (BG && rgb && inside) {
+            // background pixels: rgb = 0 * 0 + 1 * bg (chainer rasterize.py:576); grad of bg = (1 - fg) G
+            const float fg = q.fi >= 0 ? 1.f : 0.f;
+            if (q.fi < 0) {
+                float bgc[3];
+                background(sh, b, px, py, S, bgc);
+#pragma unroll
+                for (int c = 0; c < 3; c++) I2[k][c] = fg * 0.f + (1.f - fg) * bgc[c];
+            }
+            if (a.grad_bg) {
+                float* gb = a.grad_bg + ((long long)b * 3) * S * S + (S - 1 - py) * S + (S - 1 - px);
+#pragma unroll
+                for (int c = 0; c < 3; c++) gb[c * S * S] = (1.f - fg) * G2[k][c];
+            }
+        }
     }
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -1274,19 +1430,43 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         if (rgb) {
             TexSample s;
             const float* fuv = fuvb + q.fi * 8;
+            // lights: rgb = texture * cw, so the texture sees G * cw and cw sees G * texture
+            float Gt[3] = {G[0], G[1], G[2]};
+            float nrm[3], cw[3];
+            if (LIT) {
+                pixel_normal(sh, b, q.fi, w, nrm);
+                light_weights(sh, b, nrm, cw);
+#pragma unroll
+                for (int c = 0; c < 3; c++) Gt[c] = G[c] * cw[c];
+            }
             // bilinear: images = sum_i wt_i T_i -> textures (staged below) and weights (gw)
             float gw[4];
-            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s, G, gw);
+            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s, Gt, gw);
             r = s.rgb[0];
             gg = s.rgb[1];
             bb = s.rgb[2];
+            if (LIT) {
+                const float gcw[3] = {G[0] * r, G[1] * gg, G[2] * bb};
+                float cw2[3];
+                light_weights(sh, b, nrm, cw2, gcw, q.gn);
+                r = r * cw[0];
+                gg = gg * cw[1];
+                bb = bb * cw[2];
+            }
+            if (BG) {  // foreground: 1 * rgb + 0 * bg, as the forward computes it
+                float bgc[3];
+                background(sh, b, px, py, S, bgc);
+                r = 1.f * r + 0.f * bgc[0];
+                gg = 1.f * gg + 0.f * bgc[1];
+                bb = 1.f * bb + 0.f * bgc[2];
+            }
             q.ay = s.y1 - s.y;
             q.by = s.y - s.y0;
             q.ax = s.x1 - s.x;
             q.bx = s.x - s.x0;
-            q.grgb[0] = G[0];
-            q.grgb[1] = G[1];
-            q.grgb[2] = G[2];
+            q.grgb[0] = Gt[0];
+            q.grgb[1] = Gt[1];
+            q.grgb[2] = Gt[2];
             if (want_tex) {
                 const bool wok = fabsf(s.lo[0]) < 1e9f && fabsf(s.lo[1]) < 1e9f;
                 const int ix0 = (int)s.x0, iy0 = (int)s.y0;
@@ -1315,7 +1495,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                         float* gtg = g4b + s.idx[i] * 4;
 #pragma unroll
                         for (int ch = 0; ch < 3; ch++) {
-                            const float v = G[ch] * s.wt[i];
+                            const float v = Gt[ch] * s.wt[i];
                             if (v != 0.f) unsafeAtomicAdd(gtg + ch, v);
                         }
                     }
@@ -1415,7 +1595,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             const int hf = fimb[hpy * S + hpx];
             Face ff = empty_face();
             if (hf >= 0) ff = load_face_rec(frb + hf * FACE_REC);
-            shade_pixel(sh, b, hf, ff, pix_center(hpx, S), pix_center(hpy, S), hI);
+            shade_pixel(sh, b, hf, ff, hpx, hpy, S, hI);
             upstream_grad(a, gimb, C, hpy, hpx, S, hG);
         }
         const int hl = hy * HW_ + hx;
@@ -1482,6 +1662,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         reinterpret_cast<float4*>(r)[1] = make_float4(__int_as_float(P[k].pos), P[k].grgb[0], P[k].grgb[1], P[k].grgb[2]);
 #pragma unroll
         for (int j = 0; j < 9; j++) r[8 + j] = gF[k][j];
+        if (LIT) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                r[17 + j] = P[k].gn[j];
+                r[20 + j] = P[k].w[j];
+            }
+        }
     }
     // output lane roles: texel t = lane & 15 of the face's 4x4 window (dx = t & 3, dy = t >> 2), member
     // chunk c = lane >> 4: lane (t, c) sums the 3 channel contributions to texel t (and, for t < 9,
@@ -1490,6 +1677,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const int tt = lane & 15, chunk = lane >> 4;
     const int tdx = tt & 3, tdy = tt >> 2;
     const int fsel = 8 + (tt < 9 ? tt : 0);
+    const int nsel_w = 20 + (tt < 9 ? tt / 3 : 0), nsel_n = 17 + (tt < 9 ? tt % 3 : 0);
+    float* __restrict__ gNb = LIT ? a.grad_normals + (long long)b * a.F * 9 : nullptr;
     const bool act0 = P[0].fi >= 0, act1 = P[1].fi >= 0;
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
     while (p0 | p1) {
@@ -1502,7 +1691,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         const unsigned long long m1 = __ballot(act1 && P[1].fi == key) & p1;
         p0 &= ~m0;
         p1 &= ~m1;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f, an = 0.f;
         if (!(NR_ABLATE & 8)) {
             // this lane's members: row `chunk` of each 16x4 sub-block (lanes 16 chunk .. 16 chunk + 15)
             unsigned mine[2] = {(unsigned)(m0 >> (16 * chunk)) & 0xffffu, (unsigned)(m1 >> (16 * chunk)) & 0xffffu};
@@ -1521,12 +1710,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                         a2 += g2 * wt;
                     }
                     af += r[fsel];
+                    if (LIT) an += r[nsel_w] * r[nsel_n];  // corner-normal gradient tt = 3 corner + axis
                 }
             }
         }
         // reduce-scatter over the 4 member chunks (lanes t, t+16, t+32, t+48) with the gfx950 lane
         // swaps (VALU, no LDS round trip): lane (t, c) ends with the chunk total of value c
         const float v = chunk_reduce_scatter(a0, a1, a2, af);
+        if (LIT) {  // the normal gradients: a plain sum over the 4 chunks, flushed by chunk 0
+            const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(an), __float_as_uint(an), false, false);
+            const float h = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+            const auto q2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+            const float nt = __uint_as_float(q2[0]) + __uint_as_float(q2[1]);
+            if (chunk == 0 && tt < 9 && nt != 0.f) unsafeAtomicAdd(gNb + key * 9 + tt, nt);
+        }
         // ---- 4. flush this face: lane (t, c) writes channel c of texel t (c < 3) or face float t (c == 3)
         if (NR_ABLATE & 4) {
             asm volatile("" ::"v"(v));
@@ -1560,6 +1757,71 @@ __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __res
     gV[i * 3 + 2] = s2;
 }
 
+// vertex-normal backward (lights): gU[b, v] = d/du of F.normalize (rasterize.py:182) applied to the
+// gradient of n[b, v], gathered over the vertex's face corners (the gather at rasterize.py:183)
+__global__ void k_vnormal_bwd(const float* __restrict__ gN, const int32_t* __restrict__ off,
+                              const int32_t* __restrict__ ent, const float* __restrict__ vnorm,
+                              float* __restrict__ gU, int F, int V, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / V), v = (int)(i % V);
+    const float* base = gN + (long long)b * F * 9;
+    float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+    for (int e = off[v]; e < off[v + 1]; e++) {
+        const float* r = base + ent[e] * 3;  // entry = 3 f + k
+        g0 += r[0];
+        g1 += r[1];
+        g2 += r[2];
+    }
+    const float4 nv = reinterpret_cast<const float4*>(vnorm)[i];  // n = u / max(|u|, eps), |u|
+    float* o = gU + i * 3;
+    if (nv.w > 1e-12f) {
+        // d(u / |u|)/du^T g = (g - n (n . g)) / |u|
+        const float nd = (nv.x * g0 + nv.y * g1) + nv.z * g2;
+        o[0] = (g0 - nv.x * nd) / nv.w;
+        o[1] = (g1 - nv.y * nd) / nv.w;
+        o[2] = (g2 - nv.z * nd) / nv.w;
+    } else {
+        o[0] = g0 / 1e-12f;
+        o[1] = g1 / 1e-12f;
+        o[2] = g2 / 1e-12f;
+    }
+}
+
+// face-normal backward (lights): the face normal gets the gradients of its distinct vertices' sums
+// (the one-hot matmul, rasterize.py:173-179), then n = a x b with a = v1 - v0, b = v2 - v1 gives
+// dL/da = b x g, dL/db = g x a, added to the face's corner gradients gF (rasterize.py:166-170)
+__global__ void k_fnormal_bwd(const float* __restrict__ face_records, const int32_t* __restrict__ fidx,
+                              const float* __restrict__ gU, float* __restrict__ gF, int F, int V, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / F), f = (int)(i % F);
+    const int v0 = fidx[f * 3], v1 = fidx[f * 3 + 1], v2 = fidx[f * 3 + 2];
+    const float* ub = gU + (long long)b * V * 3;
+    float g[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        g[j] = ub[v0 * 3 + j];
+        if (v1 != v0) g[j] += ub[v1 * 3 + j];
+        if (v2 != v0 && v2 != v1) g[j] += ub[v2 * 3 + j];
+    }
+    const float* c = face_records + i * FACE_REC;
+    const float a0 = c[3] - c[0], a1 = c[4] - c[1], a2 = c[5] - c[2];
+    const float b0 = c[6] - c[3], b1 = c[7] - c[4], b2 = c[8] - c[5];
+    const float da0 = b1 * g[2] - b2 * g[1], da1 = b2 * g[0] - b0 * g[2], da2 = b0 * g[1] - b1 * g[0];
+    const float db0 = g[1] * a2 - g[2] * a1, db1 = g[2] * a0 - g[0] * a2, db2 = g[0] * a1 - g[1] * a0;
+    float* o = gF + i * 9;
+    o[0] -= da0;
+    o[1] -= da1;
+    o[2] -= da2;
+    o[3] += da0 - db0;
+    o[4] += da1 - db1;
+    o[5] += da2 - db2;
+    o[6] += db0;
+    o[7] += db1;
+    o[8] += db2;
+}
+
 // [Bt, HWp, 4] accumulation layout -> [Bt, 3, H, W]
 __global__ void k_tex_out(const float* __restrict__ g4, float* __restrict__ out, int HW, int HWp, long long n) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1587,6 +1849,10 @@ int validate_raster(const NrRasterArgs* a, bool need_workspace) {
         if (!a->vertices_textures || !a->faces_textures || !a->textures || !a->face_uv)
             return fail(NR_ERR_ARGS, "rgb requested without textures");
         if (a->tex_height <= 0 || a->tex_width <= 0) return fail(NR_ERR_ARGS, "bad texture size");
+        if (a->num_lights < 0) return fail(NR_ERR_ARGS, "negative light count");
+        if (a->num_lights > 0 && (!a->lights || !a->vertex_normals || !a->face_normals || !a->normal_offsets ||
+                                  !a->normal_faces))
+            return fail(NR_ERR_ARGS, "lights need lights / face_normals / vertex_normals / normal CSR buffers");
         const long long span = 2 * std::llabs(a->tex_stride_c) +
                                ((long long)a->tex_height * a->tex_width - 1) * std::llabs(a->tex_stride_p) + 1;
         if (span >= (1ll << 31)) return fail(NR_ERR_ARGS, "texture item spans 2^31 elements or more");
@@ -1611,6 +1877,17 @@ Shade make_shade(const NrRasterArgs* a) {
     sh.tv.W = a->tex_width;
     sh.face_uv = a->face_uv;
     sh.uv_bstride = a->vt_batch_stride ? (long long)a->num_faces * 8 : 0;
+    const bool rgb = (a->draw_flags & NR_DRAW_RGB) != 0;
+    sh.nl = rgb ? a->num_lights : 0;
+    sh.B = a->batch_size;
+    sh.V = a->num_vertices;
+    sh.lights = a->lights;
+    sh.vnorm = a->vertex_normals;
+    sh.fidx = a->faces;
+    sh.bg = rgb ? a->backgrounds : nullptr;
+    sh.bg_sb = a->bg_stride_b;
+    sh.bg_sc = (int)a->bg_stride_c;
+    sh.bg_sy = (int)a->bg_stride_y;
     return sh;
 }
 
@@ -1631,7 +1908,8 @@ __global__ void k_selftest_div(const float* __restrict__ a, const float* __restr
 extern "C" {
 
 const char* nr_last_error(void) { return g_err.c_str(); }
-int nr_version(void) { return 1; }
+int nr_version(void) { return 2; }
+size_t nr_raster_args_size(void) { return sizeof(NrRasterArgs); }
 
 int nr_num_channels(int draw_flags) {
     return ((draw_flags & NR_DRAW_RGB) ? 3 : 0) + ((draw_flags & NR_DRAW_SILHOUETTES) ? 1 : 0) +
@@ -1655,17 +1933,26 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         const bool rgb = ra && (ra->draw_flags & NR_DRAW_RGB);
         const int uv_items = rgb ? (ra->vt_batch_stride ? B : 1) : 0;
         ProfScope _p(P_SETUP, st);
+        const bool lit = rgb && ra->num_lights > 0;
         if (vertices)
             hipLaunchKernelGGL(k_face_setup<true>, grid, dim3(256), 0, st, vertices, faces_idx, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
-                               rgb ? ra->face_uv : nullptr, uv_items);
+                               rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr);
         else
             hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), 0, st, nullptr, nullptr, face_records, V, F, S,
-                               draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0);
+                               draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
+                               nullptr);
         int e = check_launch("k_face_setup");
         if (e) return e;
+        if (lit && V > 0) {
+            const long long nv = (long long)B * V;
+            hipLaunchKernelGGL(k_vertex_normals, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, ra->face_normals,
+                               ra->normal_offsets, ra->normal_faces, ra->vertex_normals, F, V, nv);
+            e = check_launch("k_vertex_normals");
+            if (e) return e;
+        }
     }
     {
         ProfScope _p(P_RASTER, st);
@@ -1677,8 +1964,14 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     const int s = ra->anti_aliasing ? S / 2 : S;
     {
         ProfScope _p(P_SHADE, st);
-        hipLaunchKernelGGL(k_shade, dim3((unsigned)(((long long)s * s + 255) / 256), B), dim3(256), 0, st, face_records, fim,
-                           F, S, make_shade(ra), ra->anti_aliasing, images, ra->halo);
+        const Shade sh = make_shade(ra);
+        const dim3 grid((unsigned)(((long long)s * s + 255) / 256), B);
+        switch ((sh.nl ? 1 : 0) | (sh.bg ? 2 : 0)) {
+            case 0: hipLaunchKernelGGL(k_shade<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            case 1: hipLaunchKernelGGL(k_shade<1>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            case 2: hipLaunchKernelGGL(k_shade<2>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            default: hipLaunchKernelGGL(k_shade<3>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+        }
     }
     return check_launch("k_shade");
 }
@@ -1748,10 +2041,13 @@ size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw
     return (size_t)batch_size * halo_item_floats(S, nr_num_channels(draw_flags)) * sizeof(float);
 }
 
-size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int texture_items, int tex_height,
-                                   int tex_width) {
+size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num_vertices, int texture_items,
+                                   int tex_height, int tex_width, int num_lights) {
     const size_t hwp = ((size_t)tex_height * tex_width + 3) & ~size_t(3);
-    return align_up((size_t)batch_size * num_faces * 9 * 4) + align_up((size_t)texture_items * hwp * 16);
+    size_t n = align_up((size_t)batch_size * num_faces * 9 * 4) + align_up((size_t)texture_items * hwp * 16);
+    if (num_lights > 0)
+        n += align_up((size_t)batch_size * num_faces * 9 * 4) + align_up((size_t)batch_size * num_vertices * 3 * 4);
+    return n;
 }
 
 int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float* grad_vertices, float* grad_textures,
@@ -1763,8 +2059,10 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     if (a->num_faces > 0 && (!a->vertex_offsets || !a->vertex_faces))
         return fail(NR_ERR_ARGS, "missing vertex adjacency (vertex_offsets / vertex_faces)");
     const bool rgb = (a->draw_flags & NR_DRAW_RGB) && grad_textures;
+    const bool lit = (a->draw_flags & NR_DRAW_RGB) && a->num_lights > 0;
     const int tex_items = rgb ? (a->tex_stride_b ? a->batch_size : 1) : 0;
-    const size_t need = nr_backward_workspace_bytes(a->batch_size, a->num_faces, tex_items, a->tex_height, a->tex_width);
+    const size_t need = nr_backward_workspace_bytes(a->batch_size, a->num_faces, a->num_vertices, tex_items,
+                                                    a->tex_height, a->tex_width, lit ? a->num_lights : 0);
     if (need > 0 && (!workspace || workspace_bytes < need))
         return fail(NR_ERR_WORKSPACE, "backward workspace missing or too small");
     hipStream_t st = (hipStream_t)stream;
@@ -1775,7 +2073,12 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     float* g4 = (float*)((char*)workspace + gF_bytes);
     const int HW = a->tex_height * a->tex_width;
     const int HWp = (HW + 3) & ~3;
-    if (need > 0 && hipMemsetAsync(workspace, 0, need, st) != hipSuccess) return check_launch("hipMemsetAsync");
+    const size_t g4_bytes = align_up((size_t)tex_items * (((size_t)HW + 3) & ~size_t(3)) * 16);
+    float* gN = lit ? (float*)((char*)workspace + gF_bytes + g4_bytes) : nullptr;
+    float* gU = lit ? (float*)((char*)workspace + 2 * gF_bytes + g4_bytes) : nullptr;
+    // gU is fully written by k_vnormal_bwd; the accumulators before it start at zero
+    const size_t zero_bytes = lit ? 2 * gF_bytes + g4_bytes : need;
+    if (zero_bytes > 0 && hipMemsetAsync(workspace, 0, zero_bytes, st) != hipSuccess) return check_launch("hipMemsetAsync");
     BwdArgs ba;
     ba.face_records = a->face_records;
     ba.fim = a->face_index;
@@ -1783,6 +2086,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.grad_faces = gF;
     ba.grad_tex4 = rgb ? g4 : nullptr;
     ba.halo = a->halo;
+    ba.grad_normals = gN;
+    ba.grad_bg = (a->draw_flags & NR_DRAW_RGB) && a->backgrounds ? a->grad_backgrounds : nullptr;
     ba.F = a->num_faces;
     ba.aa = a->anti_aliasing;
     ba.s = a->image_size;
@@ -1793,12 +2098,31 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     Shade sh = make_shade(a);
     {
         ProfScope _p(P_BWD, st);
-        hipLaunchKernelGGL(k_raster_bwd, dim3(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size), dim3(NT), 0, st, ba,
-                           g, sh);
+        const dim3 grid(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size);
+        switch ((lit ? 1 : 0) | (sh.bg ? 2 : 0)) {
+            case 0: hipLaunchKernelGGL(k_raster_bwd<0>, grid, dim3(NT), 0, st, ba, g, sh); break;
+            case 1: hipLaunchKernelGGL(k_raster_bwd<1>, grid, dim3(NT), 0, st, ba, g, sh); break;
+            case 2: hipLaunchKernelGGL(k_raster_bwd<2>, grid, dim3(NT), 0, st, ba, g, sh); break;
+            default: hipLaunchKernelGGL(k_raster_bwd<3>, grid, dim3(NT), 0, st, ba, g, sh); break;
+        }
     }
     e = check_launch("k_raster_bwd");
     if (e) return e;
     const long long nv = (long long)a->batch_size * a->num_vertices;
+    if (lit && nv > 0) {
+        // lights: vertex-normal gradients -> face normals -> corner gradients (added into gF)
+        hipLaunchKernelGGL(k_vnormal_bwd, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gN, a->vertex_offsets,
+                           a->vertex_faces, a->vertex_normals, gU, a->num_faces, a->num_vertices, nv);
+        e = check_launch("k_vnormal_bwd");
+        if (e) return e;
+        const long long nf = (long long)a->batch_size * a->num_faces;
+        if (nf > 0) {
+            hipLaunchKernelGGL(k_fnormal_bwd, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, a->face_records,
+                               a->faces, gU, gF, a->num_faces, a->num_vertices, nf);
+            e = check_launch("k_fnormal_bwd");
+            if (e) return e;
+        }
+    }
     if (nv > 0) {
         {
             ProfScope _p(P_VGRAD, st);

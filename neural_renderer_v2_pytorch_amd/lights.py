@@ -1,5 +1,6 @@
-"""Light records (reference lights.py:4-39).  Shading with lights is a SURVEY section 8f "next"
-row; rasterize_core raises NotImplementedError when lights are passed."""
+"""Light records (reference lights.py:4-39): same classes, attributes and defaults.  rasterize_core
+turns a list of them into per-item records for the HIP shading (NrRasterArgs.lights); gradients
+flow to the vertices through the normals, not to the light parameters."""
 import torch
 
 

@@ -12,9 +12,12 @@ Behavioural notes ("Drop-in boundary"):
   * like the reference, the wrappers set hyperparams.draw_* on the object they are given; unlike
     the reference, rasterize_core does NOT double hyperparams.image_size in place under
     anti-aliasing (rasterize.py:227-228 compounds on every reuse of the object);
-  * lights (rasterize.py:252-283) and backgrounds (:208-226, :286-288) raise NotImplementedError
-    (SURVEY.md section 8f "next" rows; the reference's own blend_backgrounds raises AttributeError
-    at rasterize.py:157);
+  * lights (rasterize.py:252-283) are shaded on the GPU, forward and backward (gradients reach the
+    vertices through the smooth normal map; light parameters themselves take no gradient);
+  * backgrounds / background_color (rasterize.py:208-226, 286-288) blend with the semantics of
+    neural_renderer_chainer/rasterize.py:574-577, since the torch blend_backgrounds raises
+    AttributeError (rasterize.py:157); background_color gives zeros * colour = black, as both
+    references compute it;
   * gradients flow to vertices and textures; a vertices_textures tensor that requires grad is
     rejected (NotImplementedError) rather than silently given no gradient.
 """
@@ -164,12 +167,60 @@ def _vertex_adjacency(faces_i32, V):
     return off, ent
 
 
+_normal_adj = {}
+
+
+def _normal_adjacency(faces_i32, V):
+    """CSR vertex -> its distinct faces, ascending (the one-hot [F, V] matrix of
+    rasterize.py:173-179: a face counts once per vertex), cached per faces tensor."""
+    key = (faces_i32.data_ptr(), faces_i32._version, faces_i32.shape[0], V, faces_i32.device)
+    hit = _normal_adj.get("faces")
+    if hit is not None and hit[0] == key:
+        return hit[1], hit[2]
+    import numpy as np
+    f = faces_i32.cpu().numpy().astype(np.int64)
+    F = f.shape[0]
+    pairs = np.unique(np.stack([f.reshape(-1), np.repeat(np.arange(F), 3)], 1), axis=0)  # sorted by (v, f)
+    counts = np.bincount(pairs[:, 0], minlength=V)
+    offsets = np.zeros(V + 1, np.int32)
+    np.cumsum(counts, out=offsets[1:])
+    off = torch.as_tensor(offsets, device=faces_i32.device)
+    ent = torch.as_tensor(pairs[:, 1].astype(np.int32), device=faces_i32.device)
+    _normal_adj["faces"] = (key, off, ent, faces_i32)
+    return off, ent
+
+
+def _light_records(lights, B, dev):
+    """lights (reference Light objects, lights.py:4-39, in list order) -> [L, B, NR_LIGHT_FLOATS]
+    records for NrRasterArgs.lights: kind, backside, colour rgb, direction xyz / specular alpha."""
+    kinds = {"AmbientLight": _lib.NR_LIGHT_AMBIENT, "DirectionalLight": _lib.NR_LIGHT_DIRECTIONAL,
+             "SpecularLight": _lib.NR_LIGHT_SPECULAR}
+    recs = torch.zeros((len(lights), B, _lib.NR_LIGHT_FLOATS), dtype=torch.float32, device=dev)
+    for i, L in enumerate(lights):
+        kind = next((k for c, k in kinds.items() if any(t.__name__ == c for t in type(L).__mro__)), None)
+        if kind is None:
+            raise TypeError("unknown light type %s" % type(L).__name__)
+        parts = [L.color] + ([L.direction] if kind == _lib.NR_LIGHT_DIRECTIONAL else []) + \
+                ([L.alpha] if kind == _lib.NR_LIGHT_SPECULAR else [])
+        if any(torch.is_tensor(t) and t.requires_grad for t in parts):
+            raise NotImplementedError("gradients w.r.t. light parameters are not implemented")
+        recs[i, :, 0] = float(kind)
+        recs[i, :, 1] = float(bool(getattr(L, "backside", False)))
+        recs[i, :, 2:5] = torch.as_tensor(L.color, dtype=torch.float32, device=dev).reshape(-1, 3).expand(B, 3)
+        if kind == _lib.NR_LIGHT_DIRECTIONAL:
+            recs[i, :, 5:8] = torch.as_tensor(L.direction, dtype=torch.float32, device=dev).reshape(-1, 3).expand(B, 3)
+        elif kind == _lib.NR_LIGHT_SPECULAR:
+            recs[i, :, 5] = torch.as_tensor(L.alpha, dtype=torch.float32, device=dev).reshape(-1).expand(B)
+    return recs
+
+
 class _Cfg:
     __slots__ = ("image_size", "aa", "backside", "flags", "near", "far", "eps", "C", "V", "F", "tex_shared",
                  "tex_hw", "vt_shared", "Vt", "B", "tex_view")
 
 
-def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj=None, halo=None):
+def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj=None, halo=None, light=None,
+          bg=None):
     a = _lib.NrRasterArgs()
     a.batch_size = cfg.B
     a.num_vertices = cfg.V
@@ -207,6 +258,14 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj
         a.tex_stride_b, a.tex_stride_c, a.tex_stride_p = tv[1], tv[2], tv[3]
         a.tex_height, a.tex_width = cfg.tex_hw
         a.face_uv = face_uv.data_ptr()
+        if light is not None:  # (records, face_normals, vertex_normals, normal CSR offsets, faces)
+            a.num_lights = light[0].shape[0]
+            a.lights, a.face_normals, a.vertex_normals = light[0].data_ptr(), light[1].data_ptr(), light[2].data_ptr()
+            a.normal_offsets, a.normal_faces = light[3].data_ptr(), light[4].data_ptr()
+        if bg is not None:  # (backgrounds [B, 3, S, S] x-contiguous, grad_backgrounds or None)
+            a.backgrounds = bg[0].data_ptr()
+            a.bg_stride_b, a.bg_stride_c, a.bg_stride_y = bg[0].stride(0), bg[0].stride(1), bg[0].stride(2)
+            a.grad_backgrounds = bg[1].data_ptr() if bg[1] is not None else None
     return a
 
 
@@ -220,7 +279,7 @@ class Rasterize(torch.autograd.Function):
     images [B, C, s, s]; backward returns d/dvertices and d/dtextures."""
 
     @staticmethod
-    def forward(ctx, vertices, textures, vertices_textures, faces, faces_textures, cfg):
+    def forward(ctx, vertices, textures, vertices_textures, faces, faces_textures, backgrounds, light_recs, cfg):
         dev = vertices.device
         B = cfg.B
         S = cfg.image_size * (2 if cfg.aa else 1)
@@ -239,13 +298,20 @@ class Rasterize(torch.autograd.Function):
         if _HALO_CACHE and any(ctx.needs_input_grad[:2]):
             halo = torch.empty(L.nr_halo_bytes(B, cfg.image_size, int(cfg.aa), cfg.flags) // 4, dtype=torch.float32,
                                device=dev)
+        light = None
+        if light_recs is not None:
+            nadj = _normal_adjacency(faces, cfg.V)
+            light = (light_recs, torch.empty((B, cfg.F, 3), dtype=torch.float32, device=dev),
+                     torch.empty((B, cfg.V, 4), dtype=torch.float32, device=dev), nadj[0], nadj[1])
+        bg = (backgrounds, None) if backgrounds is not None else None
         a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws,
-                  halo=halo)
+                  halo=halo, light=light, bg=bg)
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_forward(a, _lib.ptr(images), _lib.stream_of(vertices)), "nr_rasterize_forward")
         ctx.cfg = cfg
+        ctx.light = light
         ctx.save_for_backward(vertices, textures, vertices_textures, faces, faces_textures, face_records, face_uv,
-                              fim, halo)
+                              fim, halo, backgrounds)
         ctx.mark_non_differentiable(fim)
         # no zero-filled gradient for the int32 face-index output (a 67 MB fill per backward at the
         # headline size otherwise)
@@ -255,9 +321,9 @@ class Rasterize(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_images, _grad_fim):
         cfg = ctx.cfg
-        vertices, textures, vt, faces, ft, face_records, face_uv, fim, halo = ctx.saved_tensors
+        vertices, textures, vt, faces, ft, face_records, face_uv, fim, halo, backgrounds = ctx.saved_tensors
         if grad_images is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         grad_images = grad_images.contiguous()
         L = _lib.lib()
         dev = vertices.device
@@ -270,9 +336,15 @@ class Rasterize(torch.autograd.Function):
             tex_items = 1 if cfg.tex_shared else cfg.B
             gt = torch.empty((tex_items, 3, H, W), dtype=torch.float32, device=dev)
         H, W = cfg.tex_hw
-        ws = torch.empty(L.nr_backward_workspace_bytes(cfg.B, cfg.F, tex_items, H, W), dtype=torch.uint8, device=dev)
+        nl = ctx.light[0].shape[0] if ctx.light is not None else 0
+        ws = torch.empty(L.nr_backward_workspace_bytes(cfg.B, cfg.F, cfg.V, tex_items, H, W, nl), dtype=torch.uint8,
+                         device=dev)
         adj = _vertex_adjacency(faces, cfg.V)
-        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo)
+        gbg = None
+        if backgrounds is not None and ctx.needs_input_grad[5]:
+            gbg = torch.empty((cfg.B, 3) + tuple(backgrounds.shape[2:]), dtype=torch.float32, device=dev)
+        bg = (backgrounds, gbg) if backgrounds is not None else None
+        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo, ctx.light, bg)
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),
                                                ws.numel(), _lib.stream_of(vertices)), "nr_rasterize_backward")
@@ -280,7 +352,7 @@ class Rasterize(torch.autograd.Function):
             # the Function's texture input is [B, 3, H, W], or the single [3, H, W] / [1, 3, H, W]
             # source of a shared texture (see rasterize_core): same element count as gt either way
             gt = gt.reshape(textures.shape)
-        return (gv if ctx.needs_input_grad[0] else None), gt, None, None, None, None
+        return (gv if ctx.needs_input_grad[0] else None), gt, None, None, None, gbg, None, None
 
 
 def _flags(hp):
@@ -309,11 +381,12 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
         assert params.backgrounds.shape[1] == 3
         side = hyperparams.image_size * (2 if hyperparams.anti_aliasing else 1)
         assert params.backgrounds.shape[2] == side and params.backgrounds.shape[3] == side
-    if params.lights is not None and hyperparams.draw_rgb:
-        raise NotImplementedError("lights (rasterize.py:252-283) are not implemented on the MI355X path yet")
-    if (params.backgrounds is not None or params.background_color is not None) and hyperparams.draw_rgb:
-        raise NotImplementedError("background blending (rasterize.py:156-159, 286-288) is not implemented; the "
-                                  "reference's torch blend_backgrounds raises AttributeError there")
+    if params.background_color is not None:
+        # rasterize.py:208-214 (and chainer rasterize.py:649-655): zeros * colour, i.e. black
+        side = hyperparams.image_size * (2 if hyperparams.anti_aliasing else 1)
+        params.backgrounds = torch.zeros((vertices.shape[0], 3, side, side), dtype=torch.float32,
+                                         device=vertices.device) * \
+            torch.as_tensor(params.background_color, dtype=torch.float32, device=vertices.device)[None, :, None, None]
     flags = _flags(hyperparams)
     if flags == 0:
         raise Exception  # rasterize.py:309-310
@@ -382,7 +455,19 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
     if vt is None:
         vt = torch.empty(0, device=dev)
         ft = torch.empty(0, dtype=torch.int32, device=dev)
-    images, fim = Rasterize.apply(v, tex, vt, fi, ft, cfg)
+    bg = light_recs = None
+    if hyperparams.draw_rgb:
+        # backgrounds / lights only change the rgb channels (rasterize.py:252-288); otherwise the
+        # reference validates and ignores them
+        if params.backgrounds is not None:
+            bg = params.backgrounds
+            _lib.require_gpu(bg)
+            bg = bg.float()
+            if bg.stride(3) != 1:
+                bg = bg.contiguous()
+        if params.lights is not None and len(params.lights) > 0:
+            light_recs = _light_records(params.lights, cfg.B, dev)
+    images, fim = Rasterize.apply(v, tex, vt, fi, ft, bg, light_recs, cfg)
     if return_face_index:
         return images, fim
     return images

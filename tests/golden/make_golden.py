@@ -250,9 +250,78 @@ def scene_edges():
     save("edges", **out)
 
 
+def _light_arrays(lights):
+    """Light objects -> plain arrays for the fixture: kind 0 ambient, 1 directional, 2 specular."""
+    kinds, colors, dirs, alphas, backs = [], [], [], [], []
+    for L in lights:
+        kind = {"AmbientLight": 0, "DirectionalLight": 1, "SpecularLight": 2}[type(L).__name__]
+        kinds.append(kind)
+        colors.append(L.color.detach().numpy())
+        dirs.append(L.direction.detach().numpy() if kind == 1 else np.zeros_like(L.color.numpy()))
+        alphas.append(L.alpha.detach().numpy() if kind == 2 else np.ones(L.color.shape[0], np.float32))
+        backs.append(int(getattr(L, "backside", False)))
+    return dict(light_kind=np.asarray(kinds, np.int32), light_color=np.stack(colors),
+                light_direction=np.stack(dirs), light_alpha=np.stack(alphas), light_backside=np.asarray(backs, np.int32))
+
+
+def _lit(name, ren_fn, proj, f, vt, ft, tex_np, lights, image_size, aa, draw_backside, seed, shared_tex=True):
+    """A textured render with lights through the reference's rasterize_* (lights loop
+    rasterize.py:252-283, compute_normal_map :162-190), forward and backward."""
+    B = proj.shape[0]
+    tex_leaf = torch.as_tensor(tex_np).requires_grad_(True)
+    textures = tex_leaf[None].expand((B,) + tex_leaf.shape) if shared_tex else tex_leaf
+    vts = torch.as_tensor(vt)[None].expand((B,) + vt.shape)
+    params = RP.RasterizeParam(vertices_textures=vts, faces_textures=torch.as_tensor(ft), textures=textures,
+                               lights=lights)
+    hp = RP.RasterizeHyperparam(image_size=image_size, anti_aliasing=aa, draw_backside=draw_backside)
+    leaf, img = flags_call(ren_fn, proj, f, params, hp)
+    g = torch.as_tensor(np.random.RandomState(seed).normal(size=img.shape).astype(np.float32))
+    img.backward(g)
+    save(name, proj=proj, faces=f, vertices_textures=vt, faces_textures=ft, textures=tex_np,
+         shared_textures=np.int32(shared_tex), image_size=np.int32(image_size), anti_aliasing=np.int32(aa),
+         draw_backside=np.int32(draw_backside), images=img, grad_up=g, grad_proj=leaf.grad,
+         grad_textures=tex_leaf.grad, **_light_arrays(lights))
+
+
+def scene_lights():
+    Lm = R.lights
+    # tests_torch/test_rasterize.py:158-200 (test_forward_case4): teapot in slot 2 of 4, three lights,
+    # no backside, render_rgb; here at 96^2 output, with a random texture atlas and the backward
+    vb, f = teapot_batch()
+    eye = R.utils.get_points_from_angles(2.732, 30, 30)
+    proj = R.perspective(R.look_at(torch.as_tensor(vb), eye))
+    vt, ft, tex = R.utils.create_textures(f.shape[0], texture_size=4)
+    tex = np.random.RandomState(5).uniform(0, 1, tex.shape).astype(np.float32)
+    c1 = torch.as_tensor([[0.47481096, 0.7131511, 0.4510043], [0.49120015, 0.161955, 0.71638113],
+                          [0.32655084, 0.7805874, 0.7682426], [0.42193118, 0.90416473, 0.5267034]])
+    d1 = torch.as_tensor([[0.328245, 0.8916046, 0.31189483], [0.99824226, 0.05838178, 0.00867782],
+                          [0.35747865, 0.61983925, 0.6985467], [0.0393897, 0.6937492, 0.7191179]])
+    c2 = torch.as_tensor([[0.2732121, 0.09439224, 0.38380036], [0.06487979, 0.02794903, 0.261018],
+                          [0.28739947, 0.2996951, 0.42412606], [0.10019363, 0.26517034, 0.07372955]])
+    c3 = torch.as_tensor([[0.32410273, 0.24369295, 0.3126097], [0.3456873, 0.24514836, 0.21663068],
+                          [0.33004418, 0.25533527, 0.48039845], [0.29468802, 0.44377372, 0.10724097]])
+    lights = [Lm.DirectionalLight(c1, d1), Lm.AmbientLight(c2), Lm.SpecularLight(c3)]
+    _lit("teapot_lights", R.rasterize_rgb, proj, f, vt, ft, tex, lights, 96, True, False, 41)
+    # every light kind and option (backside, specular alpha), all channels, per-item light values
+    v, fi = synthetic.icosphere(2)
+    B = 2
+    vb = synthetic.jittered(v, B)
+    eyes = synthetic.viewpoints(B)
+    proj = torch.cat([R.perspective(R.look_at(torch.as_tensor(vb[b:b + 1]), torch.as_tensor(eyes[b:b + 1])))
+                      for b in range(B)], 0)
+    vt, ft, tex = R.utils.create_textures(fi.shape[0], texture_size=4)
+    tex = np.random.RandomState(6).uniform(0, 1, tex.shape).astype(np.float32)
+    r = np.random.RandomState(7)
+    col = lambda: torch.as_tensor(r.uniform(0.1, 0.6, (B, 3)).astype(np.float32))
+    dirn = lambda: torch.nn.functional.normalize(torch.as_tensor(r.normal(size=(B, 3)).astype(np.float32)), dim=1)
+    lights = [Lm.AmbientLight(col()), Lm.DirectionalLight(col(), dirn()), Lm.DirectionalLight(col(), dirn(), backside=True),
+              Lm.SpecularLight(col(), alpha=torch.as_tensor([2.5, 0.7])), Lm.SpecularLight(col(), backside=True)]
+    _lit("ico_lights", rasterize_all, proj, fi, vt, ft, tex, lights, 40, True, True, 42)
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
     todo = sys.argv[1:] or ["square", "teapot_sil", "teapot_depth", "teapot_textured", "ico", "car",
-                            "diff_kat", "edges"]
+                            "diff_kat", "edges", "lights"]
     for name in todo:
         globals()["scene_" + name]()

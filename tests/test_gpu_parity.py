@@ -416,8 +416,8 @@ def test_exact_division_shortcut(dev):
     assert not bad.any(), (int(bad.sum()), a[bad][:4].tolist(), b[bad][:4].tolist())
 
 
-@pytest.mark.parametrize("aa,size", [(True, 64), (False, 70)])
-def test_halo_cache_matches_reshading(dev, aa, size):
+@pytest.mark.parametrize("aa,size,extras", [(True, 64, False), (False, 70, False), (True, 48, True)])
+def test_halo_cache_matches_reshading(dev, aa, size, extras):
     """The backward's tile halos read from the forward's halo cache give the same gradients as
     re-shading them (NrRasterArgs.halo NULL); includes a size that is not a multiple of the tiles."""
     B = 3
@@ -431,9 +431,15 @@ def test_halo_cache_matches_reshading(dev, aa, size):
         try:
             pv = proj.to(dev).requires_grad_(True)
             tx = tex.clone().requires_grad_(True)
+            S = size * (2 if aa else 1)
+            extra = {}
+            if extras:  # lights and backgrounds change the halo's image values too
+                extra = dict(backgrounds=torch.rand((B, 3, S, S), generator=torch.Generator().manual_seed(2)).to(dev),
+                             lights=[nr.AmbientLight(torch.full((B, 3), 0.4, device=dev)),
+                                     nr.SpecularLight(torch.full((B, 3), 0.5, device=dev))])
             params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
                                        faces_textures=torch.as_tensor(ft, device=dev),
-                                       textures=tx[None].expand(B, -1, -1, -1))
+                                       textures=tx[None].expand(B, -1, -1, -1), **extra)
             img = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params,
                                      nr.RasterizeHyperparam(image_size=size, anti_aliasing=aa))
             img.backward(g)
@@ -443,3 +449,100 @@ def test_halo_cache_matches_reshading(dev, aa, size):
     assert torch.equal(grads[0][0], grads[1][0])
     close_grads(grads[0][1], grads[1][1], "grad vertices")
     close_grads(grads[0][2], grads[1][2], "grad textures")
+
+
+def _fixture_lights(d, dev):
+    """Our light classes from a golden fixture's light arrays (kind 0 ambient, 1 directional, 2 specular)."""
+    out = []
+    for i, k in enumerate(d["light_kind"]):
+        col = torch.as_tensor(d["light_color"][i], device=dev)
+        if k == 0:
+            out.append(nr.AmbientLight(col))
+        elif k == 1:
+            out.append(nr.DirectionalLight(col, torch.as_tensor(d["light_direction"][i], device=dev),
+                                           backside=bool(d["light_backside"][i])))
+        else:
+            out.append(nr.SpecularLight(col, alpha=torch.as_tensor(d["light_alpha"][i], device=dev),
+                                        backside=bool(d["light_backside"][i])))
+    return out
+
+
+@pytest.mark.parametrize("name", ["teapot_lights", "ico_lights"])
+def test_lights_golden(golden, dev, name):
+    """Lit textured renders (rasterize.py:162-190 normal map, 252-283 light loop) against the
+    reference's own images and gradients: the teapot scene of tests_torch/test_rasterize.py
+    test_forward_case4 (three lights, no backside) and every light kind / option on an ico-sphere."""
+    d = golden(name)
+    B = d["proj"].shape[0]
+    pv = torch.as_tensor(d["proj"], device=dev).requires_grad_(True)
+    tex = torch.as_tensor(d["textures"], device=dev).requires_grad_(True)
+    chans = d["images"].shape[1]
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(d["vertices_textures"], device=dev)[None].expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(d["faces_textures"], device=dev),
+                               textures=tex[None].expand(B, -1, -1, -1), lights=_fixture_lights(d, dev))
+    hp = nr.RasterizeHyperparam(image_size=int(d["image_size"]), anti_aliasing=bool(d["anti_aliasing"]),
+                                draw_backside=bool(d["draw_backside"]), draw_silhouettes=chans == 5, draw_depth=chans == 5)
+    img = nrr.rasterize_core(pv, torch.as_tensor(d["faces"], device=dev), params, hp)
+    close_images(img, d["images"], name + " images")
+    img.backward(torch.as_tensor(d["grad_up"], device=dev))
+    close_grads(pv.grad, d["grad_proj"], name + " grad vertices")
+    close_grads(tex.grad, d["grad_textures"], name + " grad textures")
+
+
+@pytest.mark.parametrize("aa,size,lit", [(True, 40, False), (False, 50, True)])
+def test_backgrounds_vs_oracle(oracle_mod, dev, aa, size, lit):
+    """backgrounds blended with the chainer semantics (rasterize.py:574-577; the torch
+    blend_backgrounds raises, so this is pinned by the oracle restatement only): images and the
+    gradients of vertices, textures and the backgrounds themselves, with and without lights."""
+    B = 2
+    proj, f = _ico_batch(2, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.rand(tex.shape, generator=torch.Generator().manual_seed(8))
+    S = size * (2 if aa else 1)
+    bgs = torch.rand((B, 3, S, S), generator=torch.Generator().manual_seed(9))
+    lights_cpu = [nr.AmbientLight(torch.full((B, 3), 0.3)),
+                  nr.DirectionalLight(torch.full((B, 3), 0.6), torch.tensor([[0.3, -0.5, 0.81]] * B))] if lit else None
+    g = torch.randn((B, 5, size, size), generator=torch.Generator().manual_seed(10))
+    out = {}
+    for where in ("gpu", "cpu"):
+        d = dev if where == "gpu" else torch.device("cpu")
+        pv = proj.to(d).clone().requires_grad_(True)
+        tx = tex.to(d).clone().requires_grad_(True)
+        bg = bgs.to(d).clone().requires_grad_(True)
+        vts = torch.as_tensor(vt, device=d)[None].expand(B, -1, -1)
+        lights = None
+        if lit:
+            lights = [nr.AmbientLight(lights_cpu[0].color.to(d)),
+                      nr.DirectionalLight(lights_cpu[1].color.to(d), lights_cpu[1].direction.to(d))]
+        if where == "gpu":
+            params = nr.RasterizeParam(vertices_textures=vts, faces_textures=torch.as_tensor(ft, device=d),
+                                       textures=tx[None].expand(B, -1, -1, -1), backgrounds=bg, lights=lights)
+            img = nrr.rasterize_core(pv, torch.as_tensor(f, device=d), params,
+                                     nr.RasterizeHyperparam(image_size=size, anti_aliasing=aa))
+        else:
+            img = oracle_mod.rasterize_core(pv, f, image_size=size, anti_aliasing=aa, vertices_textures=vts,
+                                            faces_textures=ft, textures=tx[None].expand(B, -1, -1, -1),
+                                            lights=lights, backgrounds=bg)
+        img.backward(g.to(d))
+        out[where] = (img.detach().cpu(), pv.grad.cpu(), tx.grad.cpu(), bg.grad.cpu())
+    close_images(out["gpu"][0], out["cpu"][0], "images")
+    for i, what in ((1, "vertices"), (2, "textures"), (3, "backgrounds")):
+        close_grads(out["gpu"][i], out["cpu"][i], "grad " + what)
+
+
+def test_background_color_is_black(dev):
+    """background_color: the reference computes zeros * colour (rasterize.py:208-214), a black
+    background; the parameter object gets the backgrounds tensor, as the reference sets it."""
+    B = 1
+    proj, f = _ico_batch(2, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None],
+                               faces_textures=torch.as_tensor(ft, device=dev),
+                               textures=torch.rand((1,) + tex.shape, device=dev), background_color=[0.2, 0.5, 0.9])
+    img = nr.rasterize_rgb(proj.to(dev), torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(image_size=32))
+    plain = nr.rasterize_rgb(proj.to(dev), torch.as_tensor(f, device=dev),
+                             nr.RasterizeParam(vertices_textures=params.vertices_textures,
+                                               faces_textures=params.faces_textures, textures=params.textures),
+                             nr.RasterizeHyperparam(image_size=32))
+    assert params.backgrounds is not None and float(params.backgrounds.abs().max()) == 0
+    assert torch.equal(img, plain)

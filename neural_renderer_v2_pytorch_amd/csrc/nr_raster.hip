@@ -1693,26 +1693,33 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         p1 &= ~m1;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f, an = 0.f;
         if (!(NR_ABLATE & 8)) {
-            // this lane's members: row `chunk` of each 16x4 sub-block (lanes 16 chunk .. 16 chunk + 15)
-            unsigned mine[2] = {(unsigned)(m0 >> (16 * chunk)) & 0xffffu, (unsigned)(m1 >> (16 * chunk)) & 0xffffu};
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-                for (unsigned m = mine[k]; m; m &= m - 1) {
-                    const float* r = rec + (k * 64 + 16 * chunk + __builtin_ctz(m)) * REC;
-                    const int pos = __float_as_int(r[4]);
-                    const int cx = tdx - (pos & 0xff), cy = tdy - (pos >> 8);
-                    const bool hit = pos >= 0 && cx >= 0 && cx <= 1 && cy >= 0 && cy <= 1;
-                    const float wt = r[cy & 1] * r[2 + (cx & 1)];
-                    const float g0 = r[5], g1 = r[6], g2 = r[7];
-                    if (hit) {
-                        a0 += g0 * wt;
-                        a1 += g1 * wt;
-                        a2 += g2 * wt;
-                    }
-                    af += r[fsel];
-                    if (LIT) an += r[nsel_w] * r[nsel_n];  // corner-normal gradient tt = 3 corner + axis
+            // this lane's members: row `chunk` of each 16x4 sub-block (lanes 16 chunk .. 16 chunk + 15);
+            // bits 0..15 from the first pixel of each lane, 16..31 from the second
+            uint32_t mine = ((uint32_t)(m0 >> (16 * chunk)) & 0xffffu) | (((uint32_t)(m1 >> (16 * chunk)) & 0xffffu) << 16);
+            const float* rbase = rec + 16 * chunk * REC;
+            // one member's contribution: its loads issued together, accumulation predicated (no branch)
+            auto member = [&](int bit, bool on) {
+                const float* r = rbase + (((bit >> 4) * 64) + (bit & 15)) * REC;
+                const float4 ra = reinterpret_cast<const float4*>(r)[0];  // ay by ax bx
+                const float4 rb = reinterpret_cast<const float4*>(r)[1];  // pos G_r G_g G_b
+                const float rf = r[fsel];
+                float rw = 0.f, rn = 0.f;
+                if (LIT) {
+                    rw = r[nsel_w];
+                    rn = r[nsel_n];
                 }
-            }
+                const int pos = __float_as_int(rb.x);
+                const int cx = tdx - (pos & 0xff), cy = tdy - (pos >> 8);
+                const bool hit = on && pos >= 0 && cx >= 0 && cx <= 1 && cy >= 0 && cy <= 1;
+                const float wt = hit ? (cy & 1 ? ra.y : ra.x) * (cx & 1 ? ra.w : ra.z) : 0.f;
+                a0 += rb.y * wt;
+                a1 += rb.z * wt;
+                a2 += rb.w * wt;
+                af += on ? rf : 0.f;
+                if (LIT) an += on ? rw * rn : 0.f;  // corner-normal gradient tt = 3 corner + axis
+            };
+            // one loop over both pixel rows (2- and 4-member steps measured slower)
+            for (; mine; mine &= mine - 1) member(__builtin_ctz(mine), true);
         }
         // reduce-scatter over the 4 member chunks (lanes t, t+16, t+32, t+48) with the gfx950 lane
         // swaps (VALU, no LDS round trip): lane (t, c) ends with the chunk total of value c

@@ -1306,7 +1306,7 @@ struct BwdPix {
 
 // FEAT: 1 = lights, 2 = backgrounds (separate instantiations keep the plain path lean)
 template <int FEAT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : 4, 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
     constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0;
     // features this instantiation does not have become compile-time constants (the shared
     // shade_pixel then carries no light / background code or arguments)
@@ -1682,13 +1682,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const bool act0 = P[0].fi >= 0, act1 = P[1].fi >= 0;
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
     while (p0 | p1) {
+        // leader: lowest pending pixel; both candidates read without branches, selected on the scalar unit
         const bool from0 = p0 != 0ull;
-        const int leader = from0 ? __builtin_ctzll(p0) : __builtin_ctzll(p1);
-        const int key = from0 ? __builtin_amdgcn_readlane(P[0].fi, leader) : __builtin_amdgcn_readlane(P[1].fi, leader);
-        const int wx = from0 ? __builtin_amdgcn_readlane(P[0].wx, leader) : __builtin_amdgcn_readlane(P[1].wx, leader);
-        const int wy = from0 ? __builtin_amdgcn_readlane(P[0].wy, leader) : __builtin_amdgcn_readlane(P[1].wy, leader);
-        const unsigned long long m0 = __ballot(act0 && P[0].fi == key) & p0;
-        const unsigned long long m1 = __ballot(act1 && P[1].fi == key) & p1;
+        const int l0 = from0 ? __builtin_ctzll(p0) : 0, l1 = p1 ? __builtin_ctzll(p1) : 0;
+        const int k0 = __builtin_amdgcn_readlane(P[0].fi, l0), k1 = __builtin_amdgcn_readlane(P[1].fi, l1);
+        const int x0w = __builtin_amdgcn_readlane(P[0].wx, l0), x1w = __builtin_amdgcn_readlane(P[1].wx, l1);
+        const int y0w = __builtin_amdgcn_readlane(P[0].wy, l0), y1w = __builtin_amdgcn_readlane(P[1].wy, l1);
+        const int key = from0 ? k0 : k1, wx = from0 ? x0w : x1w, wy = from0 ? y0w : y1w;
+        // key >= 0, so fi == key implies an active pixel
+        const unsigned long long m0 = __builtin_amdgcn_ballot_w64(P[0].fi == key) & p0;
+        const unsigned long long m1 = __builtin_amdgcn_ballot_w64(P[1].fi == key) & p1;
         p0 &= ~m0;
         p1 &= ~m1;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f, an = 0.f;

@@ -1737,12 +1737,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
         // ---- 4. flush this face: lane (t, c) writes channel c of texel t (c < 3) or face float t (c == 3)
         if (NR_ABLATE & 4) {
             asm volatile("" ::"v"(v));
-        } else if (chunk < 3) {
+        } else {
+            // one atomic per lane, address selected without branches
             const int x = wx + tdx, y = wy + tdy;
-            if (want_tex && v != 0.f && wx != INT_MIN && x < sh.tv.W && y < sh.tv.H)
-                unsafeAtomicAdd(g4b + (y * sh.tv.W + x) * 4 + chunk, v);
-        } else if (tt < 9) {
-            if (v != 0.f) unsafeAtomicAdd(gFb + key * 9 + tt, v);
+            const bool tex_lane = want_tex && chunk < 3 && wx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
+            const bool face_lane = chunk == 3 && tt < 9;
+            float* dst = tex_lane ? g4b + (y * sh.tv.W + x) * 4 + chunk : gFb + key * 9 + tt;
+            if ((tex_lane || face_lane) && v != 0.f) unsafeAtomicAdd(dst, v);
         }
     }
 }

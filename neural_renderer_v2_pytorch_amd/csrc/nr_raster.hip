@@ -744,7 +744,10 @@ constexpr int CAND = 512;                       // candidate ids expanded per ro
 constexpr int FCAP = 128;                       // faces staged per round
 constexpr int FREC = 8;                         // float4 per staged face
 constexpr int NSUB = (COARSE * COARSE) / NT;    // pixels per thread (4)
-constexpr int FWD_LDS_FACES = FCAP * FREC * 16 + FCAP * 16 + CAND * 4;
+#ifndef NR_FWD_SOA
+#define NR_FWD_SOA 1
+#endif
+constexpr int FWD_LDS_FACES = FCAP * FREC * 16 + (NR_FWD_SOA ? 0 : FCAP * 16) + CAND * 4;
 constexpr int FWD_LDS = FWD_LDS_FACES;
 
 #ifndef NR_FWD_SHAPE
@@ -771,22 +774,37 @@ __device__ __forceinline__ void pixel_of(int t, int k, int& lx, int& ly, int& ox
     }
 }
 
-// the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel
-__device__ __forceinline__ void face_test(const float4* e, float xp, float yp, float near, float far, float delta,
-                                          float& depth_min, int& best) {
+// NR_FWD_PF: 0 = record read on demand, test by test; 1 = the next face's first two float4 read
+// during the current face's test; 2 = the first two read together, then the rest together;
+// 3 = on-demand first two, the rest together
+#ifndef NR_FWD_PF
+#define NR_FWD_PF 0
+#endif
+// staged record layout: float4 i of staged face j at s_face[i * FST + j * FSJ]; SoA (FST = FCAP)
+// makes the staging stores lane-contiguous (an AoS record stride of 128 B is an 8-way bank conflict)
+constexpr int FST = NR_FWD_SOA ? FCAP : 1, FSJ = NR_FWD_SOA ? 1 : FREC;
+__device__ __forceinline__ void pin4(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
+// the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel; q0, q1 are
+// the record's first two float4 (loaded ahead by the caller)
+__device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1, float xp, float yp, float near, float far,
+                                          float delta, float& depth_min, int& best) {
 #if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 1
-    best += (int)e[0].x;  // timing build: no per-pixel test
+    best += (int)q0.x;  // timing build: no per-pixel test
     return;
 #endif
     // The rejections of .cu:94-126 are independent of each other (none changes the state), so their
     // order is free: the depth-bound reject .cu:124-126 goes first, as it is the cheapest and lets a
     // whole wave skip a face hidden behind what its pixels already hold.
-    const float4 q1 = e[1];
     if (depth_min < q1.z) return;
-    const float4 q0 = e[0];
     // .cu:94-97 (min/max form, exact for non-NaN faces)
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
-    const float4 q2 = e[2], q3 = e[3], q4 = e[4], q5 = e[5];
+    float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
+#if NR_FWD_PF
+    // the rest of the record in one LDS round trip (not one per test)
+    float4 q6 = e[6 * FST], q7 = e[7 * FST];
+    pin4(q2), pin4(q3), pin4(q4), pin4(q5), pin4(q6), pin4(q7);
+#endif
     const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
     // .cu:107-116
     const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
@@ -798,7 +816,9 @@ __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, f
     best = __float_as_int(q1.w);  // timing build: no division block
     return;
 #endif
-    const float4 q6 = e[6];
+#if !NR_FWD_PF
+    const float4 q6 = e[6 * FST];
+#endif
     const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
     // .cu:130-139
     float w0 = (yp * q4.w - xp * q5.x) + q5.w;
@@ -806,7 +826,9 @@ __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, f
     float w2 = (yp * q4.y - xp * q4.z) + q6.y;
     const float ws = w0 + w1 + w2;
     float zp;
-    const float4 q7 = e[7];
+#if !NR_FWD_PF
+    const float4 q7 = e[7 * FST];
+#endif
     if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
         // face coordinates and depths within [2^-20, 2^20] (or 0) bound every operand below inside
         // div_nr's exact range (DESIGN.md "Numerics"); 1/z is staged per face
@@ -838,29 +860,33 @@ __device__ __forceinline__ void face_test(const float4* e, float xp, float yp, f
 __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f, int2 bb) {
     const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
     const float x2 = c[6], y2 = c[7], z2 = c[8];
-    e[0] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
+    e[0 * FST] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
                        fmaxf(fmaxf(y0, y1), y2));
-    e[1] = make_float4(__int_as_float(bb.x), __int_as_float(bb.y), fminf(fminf(z0, z1), z2), __int_as_float(f));
-    e[2] = make_float4(x0, y0, x1, y1);
-    e[3] = make_float4(x2, y2, z0, z1);
-    e[4] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
-    e[5] = make_float4(y2 - y1, x0 - x2, y0 - y2, x1 * y2 - x2 * y1);
-    e[6] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, rcp_nr(z0), rcp_nr(z1));
+    e[1 * FST] = make_float4(__int_as_float(bb.x), __int_as_float(bb.y), fminf(fminf(z0, z1), z2), __int_as_float(f));
+    e[2 * FST] = make_float4(x0, y0, x1, y1);
+    e[3 * FST] = make_float4(x2, y2, z0, z1);
+    e[4 * FST] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
+    e[5 * FST] = make_float4(y2 - y1, x0 - x2, y0 - y2, x1 * y2 - x2 * y1);
+    e[6 * FST] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, rcp_nr(z0), rcp_nr(z1));
     const bool ok = coord_ok(x0) && coord_ok(y0) && coord_ok(x1) && coord_ok(y1) && coord_ok(x2) && coord_ok(y2) &&
                     in_range(z0, 0x1p-20f, 0x1p20f) && in_range(z1, 0x1p-20f, 0x1p20f) &&
                     in_range(z2, 0x1p-20f, 0x1p20f);
-    e[7] = make_float4(rcp_nr(z2), 0.f, 0.f, __int_as_float(ok ? 1 : 0));
+    e[7 * FST] = make_float4(rcp_nr(z2), 0.f, 0.f, __int_as_float(ok ? 1 : 0));
 }
 
-__global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ face_records, int rs,
+#ifndef NR_FWD_WPE
+#define NR_FWD_WPE 8
+#endif
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
                                                   int32_t* __restrict__ fim) {
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[FWD_LDS];
     __shared__ int s_scan[4];
-    float4(*s_face)[FREC] = reinterpret_cast<float4(*)[FREC]>(s_raw);
-    float4* s_box = reinterpret_cast<float4*>(s_raw + FCAP * FREC * 16);  // float bbox, conflict-free per-lane reads
-    int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16 + FCAP * 16);
+    float4* s_face = reinterpret_cast<float4*>(s_raw);
+    // AoS only: a copy of the float bboxes for conflict-free per-lane reads (SoA reads row 0 directly)
+    float4* s_box = reinterpret_cast<float4*>(s_raw + FCAP * FREC * 16 + CAND * 4);
+    int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
 
     const int b = blockIdx.y;
     const int S = g.S;
@@ -913,8 +939,8 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
                 const int n = min(FCAP, nc - j0);
                 if (t < n) {
                     const int f = s_cand[j0 + t];
-                    stage_face(s_face[t], frb + f * rs, f, bbb[f]);
-                    s_box[t] = s_face[t][0];
+                    stage_face(s_face + t * FSJ, frb + f * rs, f, bbb[f]);
+                    if (!NR_FWD_SOA) s_box[t] = s_face[t * FSJ];
                 }
                 __syncthreads();
 #pragma unroll
@@ -925,13 +951,35 @@ __global__ __launch_bounds__(NT) void k_raster_fwd(const float* __restrict__ fac
                     for (int c0 = 0; c0 < n; c0 += 64) {
                         bool hit = false;
                         if (c0 + lane < n) {
-                            const float4 q0 = s_box[c0 + lane];
+                            const float4 q0 = NR_FWD_SOA ? s_face[c0 + lane] : s_box[c0 + lane];
                             hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
                         }
                         // faces touching this wave's pixels, walked in ascending order
-                        for (unsigned long long m = __ballot(hit); m; m &= m - 1)
-                            face_test(s_face[c0 + __builtin_ctzll(m)], xp[k], yp[k], near, far, delta, depth_min[k],
-                                      best[k]);
+                        unsigned long long m = __ballot(hit);
+#if NR_FWD_PF == 1
+                        // the next face's first two float4 are read while this face is tested
+                        if (m) {
+                            const float4* e = s_face + (c0 + __builtin_ctzll(m)) * FSJ;
+                            float4 q0 = e[0], q1 = e[FST];
+                            for (;;) {
+                                m &= m - 1;
+                                const float4* en = s_face + (c0 + (m ? __builtin_ctzll(m) : 0)) * FSJ;
+                                const float4 n0 = en[0], n1 = en[FST];
+                                face_test(e, q0, q1, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
+                                if (!m) break;
+                                e = en;
+                                q0 = n0;
+                                q1 = n1;
+                            }
+                        }
+#else
+                        for (; m; m &= m - 1) {
+                            const float4* e = s_face + (c0 + __builtin_ctzll(m)) * FSJ;
+                            float4 q0 = e[0], q1 = e[FST];
+                            if (NR_FWD_PF == 2) pin4(q0), pin4(q1);
+                            face_test(e, q0, q1, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
+                        }
+#endif
                     }
                 }
                 __syncthreads();
@@ -1000,7 +1048,10 @@ __device__ __forceinline__ void halo_store(float* __restrict__ halo, int b, int 
 // reference's summation order.  Kept out of the rasteriser so that kernel stays lean (registers,
 // occupancy); costs one extra read of the face-index map.
 template <int FEAT>  // 1 = lights, 2 = backgrounds, as k_raster_bwd
-__global__ __launch_bounds__(256) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
+#ifndef NR_SHADE_WPE
+#define NR_SHADE_WPE 7  // 7 waves/SIMD: 68 VGPRs, no spills (the unlit instantiations)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 1 : NR_SHADE_WPE, 8))) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
                                                int F, int S, Shade sh_in, int aa, float* __restrict__ images,
                                                float* __restrict__ halo) {
     Shade sh = sh_in;

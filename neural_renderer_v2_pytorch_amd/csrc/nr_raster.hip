@@ -1256,6 +1256,9 @@ template <bool LIT> constexpr int srec() { return LIT ? 24 : 20; }
 constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
 constexpr int BWD_LDS_HALO = 2 * MAXC * 128 * 4;  // halo staging (step 0), after the I / G planes
 template <bool LIT> constexpr int bwd_lds() {
+#ifdef NR_BWD_LDS_SMALL
+    return BWD_LDS_IG + BWD_LDS_HALO;  // timing builds with NR_ABLATE & 2 only (no record staging)
+#endif
     return BWD_LDS_IG + BWD_LDS_HALO > 4 * 128 * srec<LIT>() * 4 ? BWD_LDS_IG + BWD_LDS_HALO : 4 * 128 * srec<LIT>() * 4;
 }
 static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
@@ -1475,10 +1478,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
 #ifndef NR_BWD_FASTDIV
         f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
 #endif
-        const bool wfast = face_weights(xp, yp, f, q.w);
+        bool wfast = false;
+        if (NR_ABLATE & 512) {
+            q.w[0] = f.x0, q.w[1] = f.y0, q.w[2] = f.z0;  // timing build: no weights
+        } else {
+            wfast = face_weights(xp, yp, f, q.w);
+        }
         const float* w = q.w;
         float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
-        if (rgb) {
+        if (rgb && !(NR_ABLATE & 128)) {
             TexSample s;
             const float* fuv = fuvb + q.fi * 8;
             // lights: rgb = texture * cw, so the texture sees G * cw and cw sees G * texture
@@ -1585,7 +1593,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
                 q.gz[j] = gzj;
             }
         }
-        if (sh.draw & NR_DRAW_DEPTH) {
+        if ((sh.draw & NR_DRAW_DEPTH) && !(NR_ABLATE & 256)) {
             dep = depth_value(f, w, wfast);
             // depth channel gradient reloaded (cache hit) rather than a runtime-indexed register array
             const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);

@@ -13,7 +13,7 @@ from .rasterize import rasterize_core, rasterize_depth, rasterize_rgb, rasterize
 from .rasterize_param import RasterizeHyperparam, RasterizeParam
 from .renderer import Renderer
 from .save_obj import save_obj
-from .utils import create_textures, get_points_from_angles, imread, to_gpu
+from .utils import create_textures, get_points_from_angles, imread, make_gif, to_gpu
 from .differentiation import differentiation
 
 __version__ = '2.0.2+mi355x.1'

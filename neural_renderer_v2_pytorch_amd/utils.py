@@ -5,6 +5,20 @@ import numpy as np
 import torch
 
 
+def make_gif(working_directory, filename):
+    """utils.py:10-15: the frames _tmp_*.png of working_directory into an animated GIF (8/100 s per
+    frame, looping), then the frames are removed.  PIL's GIF writer stands in for ImageMagick."""
+    import glob
+    import os
+    from PIL import Image
+    paths = sorted(glob.glob('%s/_tmp_*.png' % working_directory))
+    frames = [Image.open(p).convert('P') for p in paths]
+    if frames:
+        frames[0].save(filename, save_all=True, append_images=frames[1:], duration=80, loop=0)
+    for p in paths:
+        os.remove(p)
+
+
 def to_gpu(data, device=None):
     """utils.py:18-22: move array(s) to a GPU tensor."""
     if isinstance(data, (tuple, list)):

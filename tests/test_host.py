@@ -142,3 +142,16 @@ def test_reference_binding_module_checks_inputs():
         rc.compute_weight_map_c(faces, fi, torch.zeros(16, 3), 2, 4)
     with pytest.raises(NotImplementedError):
         rc.face_index_map_forward_unsafe(faces, fi, None, None, 2, 4, 0.1, 100., 1, 1e-8)
+
+
+def test_make_gif(tmp_path):
+    """utils.py:10-15: frames _tmp_*.png -> one looping GIF, frames removed."""
+    from PIL import Image
+    from neural_renderer_v2_pytorch_amd.utils import make_gif
+    for i in range(3):
+        Image.fromarray(np.full((8, 8), 80 * i, np.uint8)).save(str(tmp_path / ('_tmp_%04d.png' % i)))
+    out = str(tmp_path / 'o.gif')
+    make_gif(str(tmp_path), out)
+    g = Image.open(out)
+    assert g.n_frames == 3
+    assert not list(tmp_path.glob('_tmp_*.png'))

@@ -164,6 +164,18 @@ NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num
 NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
                                  float* grad_textures, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The gradients that only the rgb channels carry and nr_rasterize_backward does not produce, for the
+ * same forward state and upstream grad_images:
+ *   grad_vertices_textures [Bvt, Vt, 2] (Bvt = vt_batch_stride ? B : 1; the batch total when shared):
+ *     autograd of sample_textures' uv interpolation and clamps (rasterize.py:111-121) and of the
+ *     faces_textures gather (rasterize.py:246);
+ *   grad_lights [num_lights, B, NR_LIGHT_FLOATS], laid out like NrRasterArgs.lights: colour at 2..4,
+ *     direction at 5..7 (directional) or exponent alpha at 5 (specular), zero elsewhere: autograd of
+ *     the light loop (rasterize.py:252-283).
+ * Either may be NULL; those given are fully written (zeroed, then accumulated).  Needs NR_DRAW_RGB. */
+NR_API int nr_rasterize_backward_params(const NrRasterArgs* args, const float* grad_images,
+                                        float* grad_vertices_textures, float* grad_lights, void* stream);
+
 /* Diagnostics (no reference counterpart): the kernels replace some IEEE divisions by a shortened
  * form of the compiler's own division sequence inside a guarded operand range (DESIGN.md,
  * "Numerics").  This runs both forms on n operand pairs so tests can check they agree bit for bit. */

@@ -23,7 +23,7 @@ EXPORTS = [
     "nr_compute_weight_map", "nr_mask_foreground_forward", "nr_mask_foreground_backward",
     "nr_differentiation_backward", "nr_num_channels", "nr_rasterize_forward", "nr_rasterize_backward",
     "nr_backward_workspace_bytes", "nr_profile_enable", "nr_profile_read",
-    "nr_selftest_division", "nr_halo_bytes", "nr_raster_args_size",
+    "nr_selftest_division", "nr_halo_bytes", "nr_raster_args_size", "nr_rasterize_backward_params",
 ]
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
@@ -78,6 +78,7 @@ def lib():
     L.nr_rasterize_forward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p]
     L.nr_rasterize_backward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_size_t, c_void_p]
+    L.nr_rasterize_backward_params.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p]
     L.nr_backward_workspace_bytes.restype = c_size_t
     L.nr_backward_workspace_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int]
     L.nr_raster_args_size.restype = c_size_t

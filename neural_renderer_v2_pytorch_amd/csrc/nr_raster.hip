@@ -1904,6 +1904,156 @@ __global__ void k_tex_out(const float* __restrict__ g4, float* __restrict__ out,
     out[(bt * 3 + 2) * HW + p] = v.z;
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_param_bwd: the gradients of the inputs that only the rgb channels see and that the main backward
+// does not produce -- vertices_textures (UV) and the light parameters (LGT).  One thread per internal
+// pixel (a wave = 64 pixels of one row); runs only when one of them is requested.
+//   UV:  sample_textures (rasterize.py:111-121): x = min(max(pr, lo), hm) with pr = num * dt,
+//        num = sum_k (w_k uv_k) / zq_k, lo = min_k uv_k, hm = max_k uv_k - eps.  The bilinear weight
+//        gradient (as in k_raster_bwd) goes back through the two clamps (ties split in half, as
+//        torch.maximum / torch.minimum do), to pr -> uv_k through (w_k / zq_k) dt, and to the
+//        first-occurring arg-min / arg-max corner (torch's min(-2) / max(-2) backward).  Lanes of
+//        one face are summed across the wave and the leader adds the 6 corner values to
+//        grad_vt[faces_textures[f, k]] (the gather backward of rasterize.py:246).
+//   LGT: the light loop (rasterize.py:252-283) with rgb = T cw, dL/dcw = G T: per light, the colour
+//        gets s dL/dcw, a directional light's direction gets -n s'(raw) sum_c(dL/dcw_c col_c), a
+//        specular exponent gets sum_c(dL/dcw_c col_c) s^alpha log(s) (0 where s == 0, alpha >= 0, as
+//        torch's pow backward).  Wave sums, one atomic per wave and value into grad_lights, laid
+//        out like the light records [L][B][NR_LIGHT_FLOATS] (colour 2..4, direction 5..7, alpha 5).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <bool UV, bool LGT>
+__global__ __launch_bounds__(256) void k_param_bwd(BwdArgs a, Shade sh, int S, const int32_t* __restrict__ ftex,
+                                                   float* __restrict__ grad_vt, long long gvt_bstride,
+                                                   float* __restrict__ grad_lights) {
+    const int b = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool inside = p < S * S;
+    const int y = inside ? p / S : 0, x = inside ? p - y * S : 0;
+    const int fi = inside ? a.fim[(long long)b * S * S + p] : -1;
+    const int bt = sh.tv.sb ? b : 0;
+    float guv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float T[3] = {0.f, 0.f, 0.f}, G[MAXC], nrm[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < MAXC; c++) G[c] = 0.f;
+    if (fi >= 0) {
+        const float* gimb = a.grad_images + (long long)b * sh.C * (a.aa ? a.s * a.s : S * S);
+        upstream_grad(a, gimb, sh.C, y, x, S, G);
+        Face f = load_face_rec(a.face_records + ((long long)b * a.F + fi) * FACE_REC);
+        f.flags = 0;
+        float w[3];
+        face_weights(pix_center(x, S), pix_center(y, S), f, w);
+        float Gt[3] = {G[0], G[1], G[2]};
+        float cw[3];
+        if (sh.nl) {
+            pixel_normal(sh, b, fi, w, nrm);
+            light_weights(sh, b, nrm, cw);
+#pragma unroll
+            for (int c = 0; c < 3; c++) Gt[c] = G[c] * cw[c];
+        }
+        const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + fi * 8;
+        TexSample s;
+        float gw[4];
+        sample_texture(f, w, false, fuv, sh.tv, bt, sh.eps, s, Gt, gw);
+        T[0] = s.rgb[0];
+        T[1] = s.rgb[1];
+        T[2] = s.rgb[2];
+        if (UV) {
+            const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
+            const float gp[2] = {((-(gw[0] * ay) + gw[1] * ay) - gw[2] * by) + gw[3] * by,
+                                 ((-(gw[0] * ax) - gw[1] * bx) + gw[2] * ax) + gw[3] * bx};
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
+                const float g = gp[j];
+                const float to_pc = pc == hm ? g * 0.5f : (pc < hm ? g : 0.f);
+                const float to_hm = pc == hm ? g * 0.5f : (pc > hm ? g : 0.f);
+                const float to_pr = pr == lo ? to_pc * 0.5f : (pr > lo ? to_pc : 0.f);
+                const float to_lo = pr == lo ? to_pc * 0.5f : (pr < lo ? to_pc : 0.f);
+                const float gnum = to_pr * s.dt;
+                const float u[3] = {fuv[j], fuv[2 + j], fuv[4 + j]};
+                const int kmin = (u[1] < u[0] && !(u[2] < u[1])) ? 1 : ((u[2] < u[0] && u[2] < u[1]) ? 2 : 0);
+                const int kmax = (u[1] > u[0] && !(u[2] > u[1])) ? 1 : ((u[2] > u[0] && u[2] > u[1]) ? 2 : 0);
+#pragma unroll
+                for (int k = 0; k < 3; k++)
+                    guv[2 * k + j] = (gnum / s.zq[k]) * w[k] + (k == kmin ? to_lo : 0.f) + (k == kmax ? to_hm : 0.f);
+            }
+        }
+    }
+    if (UV) {
+        // group the wave's lanes by face; the leader adds the face's 6 sums to its uv vertices
+        const bool act = fi >= 0;
+        unsigned long long pend = __ballot(act);
+        float* gvb = grad_vt + (sh.uv_bstride ? (long long)b * gvt_bstride : 0);
+        while (pend) {
+            const int leader = __builtin_ctzll(pend);
+            const int key = __builtin_amdgcn_readlane(fi, leader);
+            const bool mem = act && fi == key;
+            pend &= ~__ballot(mem);
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                const float v = wave_sum(mem ? guv[q] : 0.f);
+                if (lane == leader && v != 0.f) unsafeAtomicAdd(gvb + ftex[key * 3 + q / 2] * 2 + (q & 1), v);
+            }
+        }
+    }
+    if (LGT) {
+        const bool act = fi >= 0;
+        const float gcw[3] = {G[0] * T[0], G[1] * T[1], G[2] * T[2]};
+        for (int l = 0; l < sh.nl; l++) {
+            const float* L = sh.lights + ((long long)l * sh.B + b) * NR_LIGHT_FLOATS;
+            float* gl = grad_lights + ((long long)l * sh.B + b) * NR_LIGHT_FLOATS;
+            const int kind = (int)L[0];
+            const bool back = L[1] != 0.f;
+            const float col[3] = {L[2], L[3], L[4]};
+            float gc[3], gd[3] = {0.f, 0.f, 0.f}, ga = 0.f;
+            if (kind == NR_LIGHT_AMBIENT) {
+                gc[0] = gcw[0], gc[1] = gcw[1], gc[2] = gcw[2];
+            } else {
+                const bool dirl = kind == NR_LIGHT_DIRECTIONAL;
+                const float d0 = dirl ? L[5] : 0.f, d1 = dirl ? L[6] : 0.f, d2 = dirl ? L[7] : 1.f;
+                const float raw = ((-d0) * nrm[0] + (-d1) * nrm[1]) + (-d2) * nrm[2];
+                const float sv = back ? fabsf(raw) : t_relu(raw);
+                const float ds = back ? (raw > 0.f ? 1.f : (raw < 0.f ? -1.f : 0.f)) : (raw > 0.f ? 1.f : 0.f);
+                const float gs = (gcw[0] * col[0] + gcw[1] * col[1]) + gcw[2] * col[2];
+                if (dirl) {
+#pragma unroll
+                    for (int c = 0; c < 3; c++) gc[c] = sv * gcw[c];
+                    gd[0] = gs * ds * (-nrm[0]);
+                    gd[1] = gs * ds * (-nrm[1]);
+                    gd[2] = gs * ds * (-nrm[2]);
+                } else {
+                    const float alpha = L[5];
+                    const float pw = powf(sv, alpha);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) gc[c] = pw * gcw[c];
+                    ga = (sv == 0.f && alpha >= 0.f) ? 0.f : gs * (pw * logf(sv));
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float v = wave_sum(act ? gc[c] : 0.f);
+                if (lane == 0 && v != 0.f) unsafeAtomicAdd(gl + 2 + c, v);
+            }
+            if (kind == NR_LIGHT_DIRECTIONAL) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float v = wave_sum(act ? gd[c] : 0.f);
+                    if (lane == 0 && v != 0.f) unsafeAtomicAdd(gl + 5 + c, v);
+                }
+            } else if (kind == NR_LIGHT_SPECULAR) {
+                const float v = wave_sum(act ? ga : 0.f);
+                if (lane == 0 && v != 0.f) unsafeAtomicAdd(gl + 5, v);
+            }
+        }
+    }
+}
+
 int validate_raster(const NrRasterArgs* a, bool need_workspace) {
     if (!a) return fail(NR_ERR_ARGS, "null args");
     if (a->batch_size < 0 || a->num_faces < 0 || a->num_vertices < 0 || a->image_size <= 0)
@@ -2211,6 +2361,49 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
         e = check_launch("k_tex_out");
     }
     return e;
+}
+
+int nr_rasterize_backward_params(const NrRasterArgs* a, const float* grad_images, float* grad_vertices_textures,
+                                 float* grad_lights, void* stream) {
+    int e = validate_raster(a, false);
+    if (e) return e;
+    const bool rgb = (a->draw_flags & NR_DRAW_RGB) != 0;
+    const bool uv = rgb && grad_vertices_textures, lgt = rgb && grad_lights && a->num_lights > 0;
+    if ((grad_vertices_textures || grad_lights) && !rgb) return fail(NR_ERR_ARGS, "parameter gradients need NR_DRAW_RGB");
+    if (grad_lights && a->num_lights > 0 && !a->vertex_normals) return fail(NR_ERR_ARGS, "lights need vertex_normals");
+    hipStream_t st = (hipStream_t)stream;
+    const int B = a->batch_size;
+    const long long gvt_bstride = (long long)a->num_vertices_textures * 2;
+    if (uv) {
+        const size_t n = (size_t)(a->vt_batch_stride ? B : 1) * gvt_bstride * sizeof(float);
+        if (n && hipMemsetAsync(grad_vertices_textures, 0, n, st) != hipSuccess) return check_launch("hipMemsetAsync");
+    }
+    if (lgt) {
+        const size_t n = (size_t)a->num_lights * B * NR_LIGHT_FLOATS * sizeof(float);
+        if (n && hipMemsetAsync(grad_lights, 0, n, st) != hipSuccess) return check_launch("hipMemsetAsync");
+    }
+    if (B == 0 || a->num_faces == 0 || !(uv || lgt)) return NR_OK;
+    if (!grad_images) return fail(NR_ERR_ARGS, "null grad_images");
+    const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
+    BwdArgs ba = {};
+    ba.face_records = a->face_records;
+    ba.fim = a->face_index;
+    ba.grad_images = grad_images;
+    ba.F = a->num_faces;
+    ba.aa = a->anti_aliasing;
+    ba.s = a->image_size;
+    const Shade sh = make_shade(a);  // the lights shade (cw) the uv gradient even without light gradients
+    const dim3 grid((unsigned)(((long long)S * S + 255) / 256), B);
+    if (uv && lgt)
+        hipLaunchKernelGGL((k_param_bwd<true, true>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
+                           grad_vertices_textures, gvt_bstride, grad_lights);
+    else if (uv)
+        hipLaunchKernelGGL((k_param_bwd<true, false>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
+                           grad_vertices_textures, gvt_bstride, grad_lights);
+    else
+        hipLaunchKernelGGL((k_param_bwd<false, true>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
+                           grad_vertices_textures, gvt_bstride, grad_lights);
+    return check_launch("k_param_bwd");
 }
 
 int nr_selftest_division(const float* a, const float* b, float* q_fast, float* q_ieee, long long n, void* stream) {

@@ -13,13 +13,13 @@ Behavioural notes ("Drop-in boundary"):
     the reference, rasterize_core does NOT double hyperparams.image_size in place under
     anti-aliasing (rasterize.py:227-228 compounds on every reuse of the object);
   * lights (rasterize.py:252-283) are shaded on the GPU, forward and backward (gradients reach the
-    vertices through the smooth normal map; light parameters themselves take no gradient);
+    vertices through the smooth normal map, and the light colours / directions / exponents);
   * backgrounds / background_color (rasterize.py:208-226, 286-288) blend with the semantics of
     neural_renderer_chainer/rasterize.py:574-577, since the torch blend_backgrounds raises
     AttributeError (rasterize.py:157); background_color gives zeros * colour = black, as both
     references compute it;
-  * gradients flow to vertices and textures; a vertices_textures tensor that requires grad is
-    rejected (NotImplementedError) rather than silently given no gradient.
+  * gradients flow to vertices, textures, vertices_textures, light parameters and backgrounds,
+    as the reference's autograd gives them.
 """
 import os
 
@@ -192,26 +192,29 @@ def _normal_adjacency(faces_i32, V):
 
 def _light_records(lights, B, dev):
     """lights (reference Light objects, lights.py:4-39, in list order) -> [L, B, NR_LIGHT_FLOATS]
-    records for NrRasterArgs.lights: kind, backside, colour rgb, direction xyz / specular alpha."""
+    records for NrRasterArgs.lights: kind, backside, colour rgb, direction xyz / specular alpha.
+    Built with differentiable torch ops, so the gradient Rasterize returns for the records (same
+    layout, nr_rasterize_backward_params) reaches the light tensors that require it."""
     kinds = {"AmbientLight": _lib.NR_LIGHT_AMBIENT, "DirectionalLight": _lib.NR_LIGHT_DIRECTIONAL,
              "SpecularLight": _lib.NR_LIGHT_SPECULAR}
-    recs = torch.zeros((len(lights), B, _lib.NR_LIGHT_FLOATS), dtype=torch.float32, device=dev)
-    for i, L in enumerate(lights):
+
+    def vec(t, n):
+        return torch.as_tensor(t, dtype=torch.float32).to(dev).reshape(-1, n).expand(B, n)
+
+    recs = []
+    for L in lights:
         kind = next((k for c, k in kinds.items() if any(t.__name__ == c for t in type(L).__mro__)), None)
         if kind is None:
             raise TypeError("unknown light type %s" % type(L).__name__)
-        parts = [L.color] + ([L.direction] if kind == _lib.NR_LIGHT_DIRECTIONAL else []) + \
-                ([L.alpha] if kind == _lib.NR_LIGHT_SPECULAR else [])
-        if any(torch.is_tensor(t) and t.requires_grad for t in parts):
-            raise NotImplementedError("gradients w.r.t. light parameters are not implemented")
-        recs[i, :, 0] = float(kind)
-        recs[i, :, 1] = float(bool(getattr(L, "backside", False)))
-        recs[i, :, 2:5] = torch.as_tensor(L.color, dtype=torch.float32, device=dev).reshape(-1, 3).expand(B, 3)
+        head = torch.tensor([float(kind), float(bool(getattr(L, "backside", False)))], device=dev).expand(B, 2)
         if kind == _lib.NR_LIGHT_DIRECTIONAL:
-            recs[i, :, 5:8] = torch.as_tensor(L.direction, dtype=torch.float32, device=dev).reshape(-1, 3).expand(B, 3)
+            tail = vec(L.direction, 3)
         elif kind == _lib.NR_LIGHT_SPECULAR:
-            recs[i, :, 5] = torch.as_tensor(L.alpha, dtype=torch.float32, device=dev).reshape(-1).expand(B)
-    return recs
+            tail = torch.cat([vec(L.alpha, 1), torch.zeros((B, 2), device=dev)], 1)
+        else:
+            tail = torch.zeros((B, 3), device=dev)
+        recs.append(torch.cat([head, vec(L.color, 3), tail], 1))
+    return torch.stack(recs).contiguous()
 
 
 class _Cfg:
@@ -281,6 +284,9 @@ class Rasterize(torch.autograd.Function):
     @staticmethod
     def forward(ctx, vertices, textures, vertices_textures, faces, faces_textures, backgrounds, light_recs, cfg):
         dev = vertices.device
+        ctx.vt_shape = vertices_textures.shape
+        if vertices_textures.ndim == 3 and vertices_textures.shape[0] == 1 and cfg.B > 1:
+            vertices_textures = vertices_textures.expand(cfg.B, -1, -1)  # shared: batch stride 0
         B = cfg.B
         S = cfg.image_size * (2 if cfg.aa else 1)
         L = _lib.lib()
@@ -322,6 +328,8 @@ class Rasterize(torch.autograd.Function):
     def backward(ctx, grad_images, _grad_fim):
         cfg = ctx.cfg
         vertices, textures, vt, faces, ft, face_records, face_uv, fim, halo, backgrounds = ctx.saved_tensors
+        if vt.ndim == 3 and vt.shape[0] == 1 and cfg.B > 1:
+            vt = vt.expand(cfg.B, -1, -1)
         if grad_images is None:
             return None, None, None, None, None, None, None, None
         grad_images = grad_images.contiguous()
@@ -352,7 +360,20 @@ class Rasterize(torch.autograd.Function):
             # the Function's texture input is [B, 3, H, W], or the single [3, H, W] / [1, 3, H, W]
             # source of a shared texture (see rasterize_core): same element count as gt either way
             gt = gt.reshape(textures.shape)
-        return (gv if ctx.needs_input_grad[0] else None), gt, None, None, None, gbg, None, None
+        # vertices_textures and light parameters (rasterize.py:246, 252-283): a second, separate pass
+        gvt = glt = None
+        want_vt = bool(cfg.flags & _lib.NR_DRAW_RGB) and ctx.needs_input_grad[2]
+        want_lt = bool(cfg.flags & _lib.NR_DRAW_RGB) and ctx.needs_input_grad[6] and ctx.light is not None
+        if want_vt or want_lt:
+            if want_vt:
+                # the Function's vt input is [B, Vt, 2] per item, or the [1, Vt, 2] source of a shared one
+                gvt = torch.empty(tuple(ctx.vt_shape), dtype=torch.float32, device=dev)
+            if want_lt:
+                glt = torch.empty_like(ctx.light[0])
+            with torch.cuda.device(dev):
+                _lib.check(L.nr_rasterize_backward_params(a, _lib.ptr(grad_images), _lib.ptr(gvt), _lib.ptr(glt),
+                                                          _lib.stream_of(vertices)), "nr_rasterize_backward_params")
+        return (gv if ctx.needs_input_grad[0] else None), gt, gvt, None, None, gbg, glt, None
 
 
 def _flags(hp):
@@ -412,17 +433,17 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
         vt = params.vertices_textures
         tex = params.textures
         _lib.require_gpu(vt, tex)
-        if vt.requires_grad:
-            raise NotImplementedError("gradients w.r.t. vertices_textures are not implemented")
-        vt = vt.detach().float()
+        vt = vt.float()
         if vt.shape[0] not in (1, cfg.B):
             raise AssertionError("vertices_textures batch must be 1 or %d" % cfg.B)
-        if vt.shape[0] == 1 and cfg.B > 1:
-            vt = vt.expand(cfg.B, *vt.shape[1:])
+        # the Function gets the [1, Vt, 2] source of a batch-shared vt (a slice of the expanded view,
+        # so autograd returns its gradient once, summed over the items) or the per-item [B, Vt, 2]
+        if vt.shape[0] == 1 or vt.stride(0) == 0:
+            vt = vt[:1]
         if vt.stride(2) != 1 or vt.stride(1) != 2:
             vt = vt.contiguous()
         cfg.Vt = vt.shape[1]
-        cfg.vt_shared = vt.stride(0) == 0
+        cfg.vt_shared = vt.shape[0] == 1 and cfg.B > 1
         ft = _faces_i32(params.faces_textures, dev, cfg.Vt, "faces_textures")
         if ft.shape[0] != cfg.F:
             raise AssertionError("faces_textures must have one row per face")

@@ -257,7 +257,7 @@ def _light_arrays(lights):
         kind = {"AmbientLight": 0, "DirectionalLight": 1, "SpecularLight": 2}[type(L).__name__]
         kinds.append(kind)
         colors.append(L.color.detach().numpy())
-        dirs.append(L.direction.detach().numpy() if kind == 1 else np.zeros_like(L.color.numpy()))
+        dirs.append(L.direction.detach().numpy() if kind == 1 else np.zeros_like(L.color.detach().numpy()))
         alphas.append(L.alpha.detach().numpy() if kind == 2 else np.ones(L.color.shape[0], np.float32))
         backs.append(int(getattr(L, "backside", False)))
     return dict(light_kind=np.asarray(kinds, np.int32), light_color=np.stack(colors),
@@ -317,6 +317,58 @@ def scene_lights():
     lights = [Lm.AmbientLight(col()), Lm.DirectionalLight(col(), dirn()), Lm.DirectionalLight(col(), dirn(), backside=True),
               Lm.SpecularLight(col(), alpha=torch.as_tensor([2.5, 0.7])), Lm.SpecularLight(col(), backside=True)]
     _lit("ico_lights", rasterize_all, proj, fi, vt, ft, tex, lights, 40, True, True, 42)
+
+
+def scene_param_grads():
+    """Gradients w.r.t. the vertices_textures and the light parameters (colours, directions,
+    specular exponents): the reference's autograd through sample_textures (rasterize.py:100-153,
+    the faces_textures gather at :246) and the light loop (:252-283).  Two cases: per-item uv
+    coordinates with every light kind, and uv coordinates shared by the batch (an expanded
+    [1, Vt, 2] leaf) without lights."""
+    Lm = R.lights
+    v, fi = synthetic.icosphere(2)
+    B = 2
+    vb = synthetic.jittered(v, B)
+    eyes = synthetic.viewpoints(B)
+    proj = torch.cat([R.perspective(R.look_at(torch.as_tensor(vb[b:b + 1]), torch.as_tensor(eyes[b:b + 1])))
+                      for b in range(B)], 0)
+    vt, ft, tex = R.utils.create_textures(fi.shape[0], texture_size=4)
+    tex = np.random.RandomState(8).uniform(0, 1, tex.shape).astype(np.float32)
+    r = np.random.RandomState(9)
+    # uv coordinates moved off the texel grid (a per-item jitter of up to a quarter texel)
+    # (clipped so that the bilinear +1 neighbour stays inside the atlas, where the reference indexes)
+    hw = np.asarray([tex.shape[2], tex.shape[1]], np.float32)
+    vt_items = np.clip(vt[None] + r.uniform(-0.25, 0.25, (B,) + vt.shape), 0, hw - 1.01).astype(np.float32)
+    col = lambda: torch.as_tensor(r.uniform(0.1, 0.6, (B, 3)).astype(np.float32)).requires_grad_(True)
+    dirn = lambda: torch.nn.functional.normalize(torch.as_tensor(r.normal(size=(B, 3)).astype(np.float32)),
+                                                 dim=1).detach().requires_grad_(True)
+    alpha = torch.as_tensor([1.5, 0.8]).requires_grad_(True)
+    lights = [Lm.AmbientLight(col()), Lm.DirectionalLight(col(), dirn()), Lm.DirectionalLight(col(), dirn(), backside=True),
+              Lm.SpecularLight(col(), alpha=alpha), Lm.SpecularLight(col(), backside=True)]
+    for case, (vts_np, lts) in {"param_grads_items": (vt_items, lights), "param_grads_shared": (vt_items[:1], None)}.items():
+        tex_leaf = torch.as_tensor(tex).requires_grad_(True)
+        vt_leaf = torch.as_tensor(vts_np).requires_grad_(True)
+        vts = vt_leaf if vt_leaf.shape[0] == B else vt_leaf.expand((B,) + vt_leaf.shape[1:])
+        params = RP.RasterizeParam(vertices_textures=vts, faces_textures=torch.as_tensor(ft),
+                                   textures=tex_leaf[None].expand((B,) + tex_leaf.shape), lights=lts)
+        hp = RP.RasterizeHyperparam(image_size=40, anti_aliasing=True, draw_backside=True)
+        leaf, img = flags_call(rasterize_all, proj, fi, params, hp)
+        g = torch.as_tensor(np.random.RandomState(43).normal(size=img.shape).astype(np.float32))
+        img.backward(g)
+        extra = {}
+        if lts is not None:
+            extra = _light_arrays(lts)
+            extra["grad_light_color"] = np.stack([L.color.grad.numpy() for L in lts])
+            extra["grad_light_direction"] = np.stack([L.direction.grad.numpy() if hasattr(L, "direction")
+                                                      else np.zeros((B, 3), np.float32) for L in lts])
+            # only the explicitly given exponent is a leaf (SpecularLight's default is a constant)
+            extra["light_alpha_requires_grad"] = np.asarray([int(L.alpha.requires_grad) if hasattr(L, "alpha") else 0
+                                                             for L in lts], np.int32)
+            extra["grad_light_alpha"] = np.stack([L.alpha.grad.numpy() for L in lts
+                                                  if hasattr(L, "alpha") and L.alpha.requires_grad])
+        save(case, proj=proj, faces=fi, vertices_textures=vts_np, faces_textures=ft, textures=tex,
+             image_size=np.int32(40), anti_aliasing=np.int32(1), draw_backside=np.int32(1), images=img, grad_up=g,
+             grad_proj=leaf.grad, grad_textures=tex_leaf.grad, grad_vertices_textures=vt_leaf.grad, **extra)
 
 
 if __name__ == "__main__":

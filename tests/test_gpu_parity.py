@@ -490,6 +490,46 @@ def test_lights_golden(golden, dev, name):
     close_grads(tex.grad, d["grad_textures"], name + " grad textures")
 
 
+@pytest.mark.parametrize("name", ["param_grads_items", "param_grads_shared"])
+def test_param_grads_golden(golden, dev, name):
+    """Gradients w.r.t. vertices_textures (per item, and shared by the batch through an expanded
+    [1, Vt, 2] leaf) and w.r.t. every light parameter (colours, directions, the given specular
+    exponent) against the reference's own autograd (rasterize.py:100-153, 246, 252-283), through
+    nr_rasterize_backward_params."""
+    d = golden(name)
+    B = d["proj"].shape[0]
+    pv = torch.as_tensor(d["proj"], device=dev).requires_grad_(True)
+    tex = torch.as_tensor(d["textures"], device=dev).requires_grad_(True)
+    vt = torch.as_tensor(d["vertices_textures"], device=dev).requires_grad_(True)
+    lights = None
+    if "light_kind" in d:
+        lights = _fixture_lights(d, dev)
+        for L, req in zip(lights, d["light_alpha_requires_grad"]):
+            L.color.requires_grad_(True)
+            if isinstance(L, nr.DirectionalLight):
+                L.direction.requires_grad_(True)
+            if isinstance(L, nr.SpecularLight):
+                L.alpha.requires_grad_(bool(req))
+    params = nr.RasterizeParam(vertices_textures=vt if vt.shape[0] == B else vt.expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(d["faces_textures"], device=dev),
+                               textures=tex[None].expand(B, -1, -1, -1), lights=lights)
+    hp = nr.RasterizeHyperparam(image_size=int(d["image_size"]), anti_aliasing=bool(d["anti_aliasing"]),
+                                draw_backside=bool(d["draw_backside"]))
+    img = nrr.rasterize_core(pv, torch.as_tensor(d["faces"], device=dev), params, hp)
+    close_images(img, d["images"], name + " images")
+    img.backward(torch.as_tensor(d["grad_up"], device=dev))
+    close_grads(pv.grad, d["grad_proj"], name + " grad vertices")
+    close_grads(tex.grad, d["grad_textures"], name + " grad textures")
+    close_grads(vt.grad, d["grad_vertices_textures"], name + " grad vertices_textures")
+    if lights is not None:
+        close_grads(torch.stack([L.color.grad for L in lights]), d["grad_light_color"], name + " grad light colours")
+        for i, L in enumerate(lights):
+            if isinstance(L, nr.DirectionalLight):
+                close_grads(L.direction.grad, d["grad_light_direction"][i], name + " grad light direction %d" % i)
+        close_grads(torch.stack([L.alpha.grad for L in lights if isinstance(L, nr.SpecularLight) and L.alpha.requires_grad]),
+                    d["grad_light_alpha"], name + " grad specular alpha")
+
+
 @pytest.mark.parametrize("aa,size,lit", [(True, 40, False), (False, 50, True)])
 def test_backgrounds_vs_oracle(oracle_mod, dev, aa, size, lit):
     """backgrounds blended with the chainer semantics (rasterize.py:574-577; the torch

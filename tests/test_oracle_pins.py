@@ -179,3 +179,36 @@ def test_oracle_lights_vs_reference(golden, oracle_mod, name):
     for got, ref in ((pv.grad, d["grad_proj"]), (tex.grad, d["grad_textures"])):
         scale = np.abs(ref).max()
         np.testing.assert_allclose(got.numpy(), ref, rtol=1e-4, atol=1e-4 * scale)
+
+
+@pytest.mark.parametrize("name", ["param_grads_items", "param_grads_shared"])
+def test_oracle_param_grads_vs_reference(golden, oracle_mod, name):
+    """Gradients w.r.t. vertices_textures (through sample_textures' uv interpolation and clamp,
+    rasterize.py:111-121, and the gather at :246) and w.r.t. the light colours, directions and
+    specular exponents (rasterize.py:252-283): the restatement against the reference's autograd."""
+    d = golden(name)
+    B = d["proj"].shape[0]
+    pv = torch.as_tensor(d["proj"]).requires_grad_(True)
+    tex = torch.as_tensor(d["textures"]).requires_grad_(True)
+    vt = torch.as_tensor(d["vertices_textures"]).requires_grad_(True)
+    lights = None
+    if "light_kind" in d:
+        leaf = lambda a: torch.as_tensor(a).clone().requires_grad_(True)  # noqa: E731
+        lights = fixture_lights(d, t=leaf)
+        for L, req in zip(lights, d["light_alpha_requires_grad"]):
+            L.alpha.requires_grad_(bool(req))
+    img = oracle_mod.rasterize_core(pv, d["faces"], image_size=int(d["image_size"]),
+                                    anti_aliasing=bool(d["anti_aliasing"]), draw_backside=bool(d["draw_backside"]),
+                                    vertices_textures=vt if vt.shape[0] == B else vt.expand(B, -1, -1),
+                                    faces_textures=d["faces_textures"], textures=tex[None].expand(B, -1, -1, -1),
+                                    lights=lights)
+    np.testing.assert_allclose(img.detach().numpy(), d["images"], rtol=1e-5, atol=1e-5)
+    img.backward(torch.as_tensor(d["grad_up"]))
+    pairs = [(pv.grad, d["grad_proj"]), (tex.grad, d["grad_textures"]), (vt.grad, d["grad_vertices_textures"])]
+    if lights is not None:
+        pairs.append((torch.stack([L.color.grad for L in lights]), d["grad_light_color"]))
+        pairs += [(L.direction.grad, d["grad_light_direction"][i]) for i, L in enumerate(lights)
+                  if type(L).__name__ == "DirectionalLight"]
+        pairs.append((torch.stack([L.alpha.grad for L in lights if L.alpha.requires_grad]), d["grad_light_alpha"]))
+    for got, ref in pairs:
+        np.testing.assert_allclose(got.numpy(), ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())

@@ -176,6 +176,34 @@ NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_ima
 NR_API int nr_rasterize_backward_params(const NrRasterArgs* args, const float* grad_images,
                                         float* grad_vertices_textures, float* grad_lights, void* stream);
 
+/* Camera prologue of Renderer.transform_vertices (renderer.py:27-38): look_at (look_at.py:5-44, with
+ * the default at = (0, 0, 0) / up = (0, 1, 0) or the given ones) and/or perspective
+ * (perspective.py:4-18), fused.  Cross products are per item (the reference's dim-less torch.cross
+ * mixes items at B == 3, SURVEY section 8a hazards). */
+enum { NR_CAMERA_NONE = 0, NR_CAMERA_LOOK_AT = 1 };
+typedef struct NrCameraArgs {
+    int batch_size;            /* B */
+    int num_vertices;          /* V */
+    const float* vertices;     /* [B, V, 3] world space; v_batch_stride 0 = one mesh for every item */
+    long long v_batch_stride;
+    const float* eye;          /* [B, 3] viewpoints; eye_batch_stride 0 = one eye for every item */
+    long long eye_batch_stride;
+    int mode;                  /* NR_CAMERA_* */
+    float at[3], up[3];
+    int perspective;           /* apply x / z / width, y / z / width */
+    float width;               /* tan(angle / 180 * 3.1416) in f32, as perspective.py:10-13 computes it */
+} NrCameraArgs;
+
+/* out [B, V, 3] contiguous. */
+NR_API int nr_camera_forward(const NrCameraArgs* args, float* out, void* stream);
+/* Scratch bytes of nr_camera_backward (per-item eye-gradient sums). */
+NR_API size_t nr_camera_workspace_bytes(int batch_size);
+/* grad_out [B, V, 3] -> grad_vertices [Bv, V, 3] (Bv = v_batch_stride ? B : 1, the item sum for a
+ * shared mesh) and grad_eye [Be, 3] (Be = eye_batch_stride ? B : 1); either may be NULL, those
+ * given are fully written. */
+NR_API int nr_camera_backward(const NrCameraArgs* args, const float* grad_out, float* grad_vertices,
+                              float* grad_eye, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Diagnostics (no reference counterpart): the kernels replace some IEEE divisions by a shortened
  * form of the compiler's own division sequence inside a guarded operand range (DESIGN.md,
  * "Numerics").  This runs both forms on n operand pairs so tests can check they agree bit for bit. */

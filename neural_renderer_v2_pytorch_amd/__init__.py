@@ -15,5 +15,6 @@ from .renderer import Renderer
 from .save_obj import save_obj
 from .utils import create_textures, get_points_from_angles, imread, make_gif, to_gpu
 from .differentiation import differentiation
+from .camera import camera_transform
 
 __version__ = '2.0.2+mi355x.1'

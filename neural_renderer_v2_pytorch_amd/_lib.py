@@ -24,6 +24,7 @@ EXPORTS = [
     "nr_differentiation_backward", "nr_num_channels", "nr_rasterize_forward", "nr_rasterize_backward",
     "nr_backward_workspace_bytes", "nr_profile_enable", "nr_profile_read",
     "nr_selftest_division", "nr_halo_bytes", "nr_raster_args_size", "nr_rasterize_backward_params",
+    "nr_camera_forward", "nr_camera_backward", "nr_camera_workspace_bytes",
 ]
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
@@ -49,6 +50,15 @@ class NrRasterArgs(ctypes.Structure):
     ]
 
 NR_LIGHT_AMBIENT, NR_LIGHT_DIRECTIONAL, NR_LIGHT_SPECULAR, NR_LIGHT_FLOATS = 0, 1, 2, 8
+NR_CAMERA_NONE, NR_CAMERA_LOOK_AT = 0, 1
+
+
+class NrCameraArgs(ctypes.Structure):  # include/nr_raster.h
+    _fields_ = [
+        ("batch_size", c_int), ("num_vertices", c_int), ("vertices", c_void_p), ("v_batch_stride", c_ll),
+        ("eye", c_void_p), ("eye_batch_stride", c_ll), ("mode", c_int), ("at", c_float * 3), ("up", c_float * 3),
+        ("perspective", c_int), ("width", c_float),
+    ]
 
 
 _lib = None
@@ -79,6 +89,11 @@ def lib():
     L.nr_rasterize_backward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_size_t, c_void_p]
     L.nr_rasterize_backward_params.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p]
+    L.nr_camera_forward.argtypes = [ctypes.POINTER(NrCameraArgs), c_void_p, c_void_p]
+    L.nr_camera_backward.argtypes = [ctypes.POINTER(NrCameraArgs), c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                     c_void_p]
+    L.nr_camera_workspace_bytes.restype = c_size_t
+    L.nr_camera_workspace_bytes.argtypes = [c_int]
     L.nr_backward_workspace_bytes.restype = c_size_t
     L.nr_backward_workspace_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int]
     L.nr_raster_args_size.restype = c_size_t
@@ -90,7 +105,7 @@ def lib():
     L.nr_profile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(c_float)]
     for name in EXPORTS:
         if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels", "nr_backward_workspace_bytes",
-                        "nr_halo_bytes", "nr_raster_args_size"):
+                        "nr_halo_bytes", "nr_raster_args_size", "nr_camera_workspace_bytes"):
             getattr(L, name).restype = c_int
     _lib = L
     return L

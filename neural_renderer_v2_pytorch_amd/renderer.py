@@ -1,6 +1,7 @@
 """Camera + dispatch API (reference renderer.py:7-75): same attributes, defaults and methods."""
 import math
 
+from . import camera
 from .look import look
 from .look_at import look_at
 from .perspective import perspective
@@ -25,6 +26,11 @@ class Renderer(object):
         self.far = 100
 
     def transform_vertices(self, vertices, lights=None):
+        # GPU tensors: look_at + perspective fused into one HIP launch each way (camera.py); 'look'
+        # and CPU tensors take the reference's composition of torch ops below
+        if self.camera_mode != 'look' and camera.fusable(vertices, self.viewing_angle):
+            return camera.camera_transform(vertices, self.viewpoints if self.camera_mode == 'look_at' else None,
+                                           perspective=self.perspective, angle=self.viewing_angle)
         if self.camera_mode == 'look_at':
             vertices = look_at(vertices, self.viewpoints)
         elif self.camera_mode == 'look':

@@ -9,8 +9,8 @@ of (images * G).sum()), producing d/dvertices and d/dtextures.
 
 Multi-GPU: one process per GPU (torchrun), each renders its own 64 items (batch sharding, weak
 scaling, no collective on the data path); the timed region is bracketed by barriers and the max
-over ranks is reported.  With --gather the rank images are also all-gathered over RCCL after the
-timed region and that time is reported separately.
+over ranks is reported.  With N > 1 the rank images are then all-gathered over RCCL (BASELINE cfg4:
+512 items on 8 GPUs "with RCCL gather") and that time is reported separately as gather_ms.
 
 Output: one JSON line on rank 0 (see README/DESIGN for field meanings).
 """
@@ -40,7 +40,8 @@ def parse():
     p.add_argument("--mode", choices=["rgbsd", "sil"], default="rgbsd")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--gather", action="store_true", help="also time an RCCL all_gather of the images")
+    p.add_argument("--no-gather", action="store_true",
+                   help="with N > 1, skip the RCCL all_gather of the images timed after the steps (cfg4)")
     return p.parse_args()
 
 
@@ -221,7 +222,7 @@ def main():
     value = px / elapsed / 1e6
 
     gather_ms = None
-    if args.gather and world > 1:
+    if not args.no_gather and world > 1:
         out = torch.empty((world,) + tuple(images.shape), device=dev, dtype=images.dtype)
         torch.cuda.synchronize()
         t1 = time.perf_counter()

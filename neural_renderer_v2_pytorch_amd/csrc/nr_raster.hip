@@ -539,7 +539,8 @@ __device__ __forceinline__ void xcd_tile(int L, int b, int nx, int ny, int& tx, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// block-wide exclusive scan of one int per thread (NT threads, 4 waves)
+// block-wide exclusive scan of one int per thread (NW waves)
+template <int NW = NT / 64>
 __device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int x = v;
@@ -552,7 +553,7 @@ __device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
     __syncthreads();
     int base = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < NT / 64; i++) {
+    for (int i = 0; i < NW; i++) {
         const int t = lds4[i];
         base += (i < wid) ? t : 0;
         tot += t;
@@ -725,68 +726,55 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_raster_fwd: one block per 32x32-pixel coarse bin (the bitmask granularity), 4 pixels per thread
-// (4 sub-tiles of 32x8; in each, the 4 waves own 16x4 pixel blocks).
+// k_raster_fwd<NTF>: one block per 32x32-pixel coarse bin (the bitmask granularity), split into 16
+// 8x8 pixel blocks; NTF / 64 waves, each walking 16 / (NTF / 64) of the 8x8 blocks in turn.
 //   1. the bin's bitmask words are expanded (block scan over popcounts) into the ordered list of
 //      candidate faces;
 //   2. up to FCAP candidates at a time are staged into LDS in ascending face order (one face per
 //      thread, one global load stage);
-//   3. per sub-tile, each wave ballots which staged faces touch its 16x4 pixels and walks the set
-//      bits in order (scalar loop), running the reference's per-face test for its pixel -- every
-//      pixel therefore sees its candidate faces in ascending index order, as the reference's
-//      sequential loop does (.cu:82-149), and the per-pixel state stays in registers across rounds;
+//   3. per 8x8 block, the wave ballots which staged faces' float bounding boxes meet the block's
+//      pixel-centre extent (an exact cull: such a face fails .cu:94-97 at every pixel of the block)
+//      and walks the set bits in order (scalar loop), running the reference's per-face test for its
+//      pixel -- every pixel therefore sees its candidate faces in ascending index order, as the
+//      reference's sequential loop does (.cu:82-149), and the per-pixel state stays in registers
+//      across rounds;
 //   shading and the output image are computed by k_shade.
-//   LDS face record (7 x float4):
+//   Block sizes (picked per launch, run_face_index): 256 threads = 4 waves, each walking the four 8x8
+//   blocks of a 16x16 quadrant (most per-thread work, least fixed cost per pixel: best when the grid
+//   has many bins of moderate depth, e.g. the headline); 1024 threads = 16 waves, one 8x8 block each
+//   (the bin's walks run 4x wider: small batches, where the grid is a few blocks per CU, and dense
+//   bins -- 300+ faces over one 8x8 block on a 50k-face torus -- no longer serialise on 4 waves).
+//   LDS face record, structure of arrays (float4 i of staged face j at s_face[i * FCAP + j]: the
+//   staging stores are lane-contiguous), 8 x float4:
 //     0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
-//     4: z2 A=x1-x0 B=y1-y0 C=x2-x1 | 5: D=y2-y1 E=x0-x2 F=y0-y2 k0 | 6: k1 k2 - -
+//     4: z2 A=x1-x0 B=y1-y0 C=x2-x1 | 5: D=y2-y1 E=x0-x2 F=y0-y2 k0 | 6: k1 k2 1/z0 1/z1 | 7: 1/z2 - - ok
 //   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
-constexpr int CAND = 512;                       // candidate ids expanded per round
-constexpr int FCAP = 128;                       // faces staged per round
-constexpr int FREC = 8;                         // float4 per staged face
-constexpr int NSUB = (COARSE * COARSE) / NT;    // pixels per thread (4)
-#ifndef NR_FWD_SOA
-#define NR_FWD_SOA 1
-#endif
-constexpr int FWD_LDS_FACES = FCAP * FREC * 16 + (NR_FWD_SOA ? 0 : FCAP * 16) + CAND * 4;
-constexpr int FWD_LDS = FWD_LDS_FACES;
-
-#ifndef NR_FWD_SHAPE
-#define NR_FWD_SHAPE 1
-#endif
-// pixel (lx, ly) of thread t in sub-tile k of the 32x32 bin, and the origin (ox, oy) of its wave's
-// pixel block in that sub-tile.
-//   shape 0: each sub-tile is a 32x8 strip, the 4 waves own 16x4 blocks of it;
-//   shape 1: each wave owns a 16x16 quadrant, walked as four 8x8 blocks (less block perimeter per
-//            pixel, so fewer faces overlap a wave's block).
-constexpr int WBW = NR_FWD_SHAPE ? 8 : 16, WBH = NR_FWD_SHAPE ? 8 : 4;  // wave block
-__device__ __forceinline__ void pixel_of(int t, int k, int& lx, int& ly, int& ox, int& oy) {
-    const int w = t >> 6, l = t & 63;
-    if (NR_FWD_SHAPE) {
-        ox = (w & 1) * 16 + (k & 1) * 8;
-        oy = (w >> 1) * 16 + (k >> 1) * 8;
-        lx = ox + (l & 7);
-        ly = oy + (l >> 3);
-    } else {
-        ox = (w & 1) * 16;
-        oy = (w >> 1) * 4 + TH * k;
-        lx = ox + (l & 15);
-        ly = oy + (l >> 4);
+constexpr int FREC = 8;  // float4 per staged face
+template <int NTF> struct FwdCfg {
+    static constexpr int NW = NTF / 64;                        // waves
+    static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
+    static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
+    static constexpr int FCAP = NTF >= 1024 ? 256 : 128;       // faces staged per round
+    static constexpr int LDS = FCAP * FREC * 16 + CAND * 4;
+    static_assert(NSUB == 1 || NSUB == 2 || NSUB == 4, "forward block layout");
+    // 8x8 block k of wave w: its origin (ox, oy) in the bin
+    __device__ static __forceinline__ void block_of(int w, int k, int& ox, int& oy) {
+        if (NSUB == 1) {         // 16 waves: wave w owns block (w & 3, w >> 2)
+            ox = (w & 3) * 8;
+            oy = (w >> 2) * 8;
+        } else if (NSUB == 2) {  // 8 waves: a vertical pair of blocks in quadrant w >> 1
+            ox = ((w >> 1) & 1) * 16 + (w & 1) * 8;
+            oy = (w >> 2) * 16 + k * 8;
+        } else {                 // 4 waves: the 16x16 quadrant w, walked as four 8x8 blocks
+            ox = (w & 1) * 16 + (k & 1) * 8;
+            oy = (w >> 1) * 16 + (k >> 1) * 8;
+        }
     }
-}
-
-// NR_FWD_PF: 0 = record read on demand, test by test; 1 = the next face's first two float4 read
-// during the current face's test; 2 = the first two read together, then the rest together;
-// 3 = on-demand first two, the rest together
-#ifndef NR_FWD_PF
-#define NR_FWD_PF 0
-#endif
-// staged record layout: float4 i of staged face j at s_face[i * FST + j * FSJ]; SoA (FST = FCAP)
-// makes the staging stores lane-contiguous (an AoS record stride of 128 B is an 8-way bank conflict)
-constexpr int FST = NR_FWD_SOA ? FCAP : 1, FSJ = NR_FWD_SOA ? 1 : FREC;
-__device__ __forceinline__ void pin4(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+};
 
 // the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel; q0, q1 are
-// the record's first two float4 (loaded ahead by the caller)
+// the record's first two float4 (loaded ahead by the caller); FST = the SoA stride (FCAP)
+template <int FST>
 __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1, float xp, float yp, float near, float far,
                                           float delta, float& depth_min, int& best) {
 #if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 1
@@ -799,12 +787,7 @@ __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1,
     if (depth_min < q1.z) return;
     // .cu:94-97 (min/max form, exact for non-NaN faces)
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
-    float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
-#if NR_FWD_PF
-    // the rest of the record in one LDS round trip (not one per test)
-    float4 q6 = e[6 * FST], q7 = e[7 * FST];
-    pin4(q2), pin4(q3), pin4(q4), pin4(q5), pin4(q6), pin4(q7);
-#endif
+    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
     const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
     // .cu:107-116
     const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
@@ -816,9 +799,7 @@ __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1,
     best = __float_as_int(q1.w);  // timing build: no division block
     return;
 #endif
-#if !NR_FWD_PF
     const float4 q6 = e[6 * FST];
-#endif
     const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
     // .cu:130-139
     float w0 = (yp * q4.w - xp * q5.x) + q5.w;
@@ -826,9 +807,7 @@ __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1,
     float w2 = (yp * q4.y - xp * q4.z) + q6.y;
     const float ws = w0 + w1 + w2;
     float zp;
-#if !NR_FWD_PF
     const float4 q7 = e[7 * FST];
-#endif
     if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
         // face coordinates and depths within [2^-20, 2^20] (or 0) bound every operand below inside
         // div_nr's exact range (DESIGN.md "Numerics"); 1/z is staged per face
@@ -857,6 +836,7 @@ __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1,
     }
 }
 
+template <int FST>
 __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f, int2 bb) {
     const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
     const float x2 = c[6], y2 = c[7], z2 = c[8];
@@ -877,15 +857,19 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
 #ifndef NR_FWD_WPE
 #define NR_FWD_WPE 8
 #endif
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
+#ifndef NR_FWD_FORCE_NT
+#define NR_FWD_FORCE_NT 0  // timing builds: 256 / 512 / 1024 threads for every launch
+#endif
+template <int NTF>
+__global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
                                                   int32_t* __restrict__ fim) {
-    __shared__ __attribute__((aligned(16))) unsigned char s_raw[FWD_LDS];
-    __shared__ int s_scan[4];
+    using C = FwdCfg<NTF>;
+    constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
+    __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
+    __shared__ int s_scan[C::NW];
     float4* s_face = reinterpret_cast<float4*>(s_raw);
-    // AoS only: a copy of the float bboxes for conflict-free per-lane reads (SoA reads row 0 directly)
-    float4* s_box = reinterpret_cast<float4*>(s_raw + FCAP * FREC * 16 + CAND * 4);
     int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
 
     const int b = blockIdx.y;
@@ -897,20 +881,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 
     const int by0 = bin_y * COARSE;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
-    int lx[NSUB], ly[NSUB], ox[NSUB], oy[NSUB];
     float xp[NSUB], yp[NSUB];
     float depth_min[NSUB];
     int best[NSUB];
     float xcl[NSUB], xch[NSUB], ycl[NSUB], ych[NSUB];
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
-        pixel_of(t, k, lx[k], ly[k], ox[k], oy[k]);
-        xcl[k] = pix_center(bx0 + ox[k], S);
-        xch[k] = pix_center(bx0 + ox[k] + WBW - 1, S);
-        ycl[k] = pix_center(by0 + oy[k], S);
-        ych[k] = pix_center(by0 + oy[k] + WBH - 1, S);
-        xp[k] = pix_center(bx0 + lx[k], S);
-        yp[k] = pix_center(by0 + ly[k], S);
+        int ox, oy;
+        C::block_of(wid, k, ox, oy);
+        xcl[k] = pix_center(bx0 + ox, S);
+        xch[k] = pix_center(bx0 + ox + 7, S);
+        ycl[k] = pix_center(by0 + oy, S);
+        ych[k] = pix_center(by0 + oy + 7, S);
+        xp[k] = pix_center(bx0 + ox + (lane & 7), S);
+        yp[k] = pix_center(by0 + oy + (lane >> 3), S);
         depth_min[k] = far;
         best[k] = -1;
     }
@@ -920,11 +904,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 
     const float* frb = face_records + (long long)b * F * rs;
     int32_t* __restrict__ fimb = fim + (long long)b * S * S;
 
-    for (int wbase = 0; wbase < g.nwords; wbase += NT) {
+    for (int wbase = 0; wbase < g.nwords; wbase += NTF) {
         const int w = wbase + t;
         const uint32_t bits = (w < g.nwords) ? words[w] : 0u;
         int total;
-        const int off = block_scan(__builtin_popcount(bits), total, s_scan);
+        const int off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
         for (int cbase = 0; cbase < total; cbase += CAND) {
             // expand my word's set bits into the ordered candidate list
             int r = off;
@@ -939,47 +923,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 
                 const int n = min(FCAP, nc - j0);
                 if (t < n) {
                     const int f = s_cand[j0 + t];
-                    stage_face(s_face + t * FSJ, frb + f * rs, f, bbb[f]);
-                    if (!NR_FWD_SOA) s_box[t] = s_face[t * FSJ];
+                    stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
                 }
                 __syncthreads();
 #pragma unroll
                 for (int k = 0; k < NSUB; k++) {
-                    // pixel-centre extent of this wave's block: a face whose float bounding box
-                    // misses it fails .cu:94-97 at every pixel of the block
                     const float xc0 = xcl[k], xc1 = xch[k], yc0 = ycl[k], yc1 = ych[k];
                     for (int c0 = 0; c0 < n; c0 += 64) {
                         bool hit = false;
                         if (c0 + lane < n) {
-                            const float4 q0 = NR_FWD_SOA ? s_face[c0 + lane] : s_box[c0 + lane];
+                            const float4 q0 = s_face[c0 + lane];
                             hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
                         }
                         // faces touching this wave's pixels, walked in ascending order
-                        unsigned long long m = __ballot(hit);
-#if NR_FWD_PF == 1
-                        // the next face's first two float4 are read while this face is tested
-                        if (m) {
-                            const float4* e = s_face + (c0 + __builtin_ctzll(m)) * FSJ;
-                            float4 q0 = e[0], q1 = e[FST];
-                            for (;;) {
-                                m &= m - 1;
-                                const float4* en = s_face + (c0 + (m ? __builtin_ctzll(m) : 0)) * FSJ;
-                                const float4 n0 = en[0], n1 = en[FST];
-                                face_test(e, q0, q1, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
-                                if (!m) break;
-                                e = en;
-                                q0 = n0;
-                                q1 = n1;
-                            }
+                        for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
+                            const float4* e = s_face + (c0 + __builtin_ctzll(m));
+                            const float4 q0 = e[0], q1 = e[FCAP];
+                            face_test<FCAP>(e, q0, q1, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
                         }
-#else
-                        for (; m; m &= m - 1) {
-                            const float4* e = s_face + (c0 + __builtin_ctzll(m)) * FSJ;
-                            float4 q0 = e[0], q1 = e[FST];
-                            if (NR_FWD_PF == 2) pin4(q0), pin4(q1);
-                            face_test(e, q0, q1, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
-                        }
-#endif
                     }
                 }
                 __syncthreads();
@@ -989,7 +950,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 
 
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
-        const int px = bx0 + lx[k], py = by0 + ly[k];
+        int ox, oy;
+        C::block_of(wid, k, ox, oy);
+        const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
         if (px < S && py < S) fimb[py * S + px] = best[k];
     }
 }
@@ -2376,8 +2339,22 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     }
     {
         ProfScope _p(P_RASTER, st);
-        hipLaunchKernelGGL(k_raster_fwd, dim3(g.nbins, B), dim3(NT), 0, st, face_records, vertices ? FACE_REC : 9, bbox, mask,
-                           F, g, near, far, delta, fim);
+        // block size (k_raster_fwd notes): 256 threads when the grid alone fills the chip many times
+        // over and the bins are shallow; 1024 when it does not, or when the bins are deep (F per bin
+        // at the 32x32 bin granularity as the depth proxy)
+        const long long blocks = (long long)g.nbins * B;
+        const double faces_per_bin = (double)F / g.nbins;
+        const int ntf = NR_FWD_FORCE_NT ? NR_FWD_FORCE_NT : ((blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024);
+        const int rs = vertices ? FACE_REC : 9;
+        if (ntf == 256)
+            hipLaunchKernelGGL(k_raster_fwd<256>, dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask, F, g,
+                               near, far, delta, fim);
+        else if (ntf == 512)
+            hipLaunchKernelGGL(k_raster_fwd<512>, dim3(g.nbins, B), dim3(512), 0, st, face_records, rs, bbox, mask, F, g,
+                               near, far, delta, fim);
+        else
+            hipLaunchKernelGGL(k_raster_fwd<1024>, dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox, mask, F, g,
+                               near, far, delta, fim);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra) return e;

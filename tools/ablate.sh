@@ -1,5 +1,6 @@
 # usage: VARIANTS="base NR_SWZ_W=1,NR_SWZ_H=1 NR_ABLATE=2" bash tools/ablate.sh <tag>
-# builds one library per variant (comma-separated -D defines; "base" = none) and benches each.
+# builds one library per variant (comma-separated -D defines; "base" = none) and benches each;
+# CONFIGS=cfg2,cfg3,cfg5 also times those configs (tools/bench_configs.py).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-ablate}
@@ -20,5 +21,13 @@ for V in $VARIANTS; do
   NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_$i.log 2>&1
   rc=$?; echo "$V rc=$rc: $(python -c "import json,sys; d=json.loads(open('$OUT/bench_$i.log').read().strip().splitlines()[-1]); print(d['kernels_ms'], d['ms_per_step'])")"
   if [ $rc -ne 0 ]; then exit $rc; fi
+  if [ -n "$CONFIGS" ]; then
+    NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python tools/bench_configs.py --loop-steps 20 --only $CONFIGS > $OUT/configs_$i.log 2>&1
+    rc=$?; python -c "
+import json
+for l in open('$OUT/configs_$i.log'):
+    if l.startswith('{'): d = json.loads(l); print('   ', d['config'][:5], d['ms_per_step'], d['kernels_ms'])"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+  fi
 done
 rm -rf $OUT/lib

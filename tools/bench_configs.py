@@ -1,0 +1,183 @@
+"""Time the single-GPU BASELINE.json configs other than the headline (bench.py measures that one):
+
+  cfg2  teapot.obj (2464 faces) B=4 at 256^2 (AA, 512^2 internal), rgb + silhouettes + depth
+  cfg3  ShapeNet car 4e49873... once midpoint-subdivided (14576 faces), B=64 at 256^2, textured rgba
+        with the car's own texture atlas
+  cfg5  example2-style loop: torus 250x100 (50000 faces) at 512^2 (1024^2 internal), silhouettes,
+        200 fwd+bwd steps with an Adam update of the vertices
+
+One step = rasterize_core forward + backward (cfg5: plus the Adam step), inputs resident on the GPU,
+median of the per-step times over --steps steps after --warmup.  Prints one JSON line per config.
+cfg1 is the reference's CPU-only plumbing case and cfg4 is bench.py --gpus 8.
+
+usage: python tools/bench_configs.py [--steps 20] [--warmup 5] [--loop-steps 200]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import neural_renderer_v2_pytorch_amd as nr  # noqa: E402
+from neural_renderer_v2_pytorch_amd import synthetic  # noqa: E402
+
+DATA = os.path.join(ROOT, "tests", "data")
+
+
+def subdivide(v, f, vt=None, ft=None):
+    """Midpoint subdivision: every triangle into 4 (shared edge midpoints); the same on the uv mesh."""
+    def split(verts, faces):
+        cache, out_v, nf = {}, [tuple(x) for x in verts], []
+
+        def mid(a, b):
+            key = (min(a, b), max(a, b))
+            if key not in cache:
+                out_v.append(tuple((np.asarray(out_v[a], np.float64) + np.asarray(out_v[b], np.float64)) / 2))
+                cache[key] = len(out_v) - 1
+            return cache[key]
+        for a, b, c in faces:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            nf += [(a, ab, ca), (b, bc, ab), (c, ca, bc), (ab, bc, ca)]
+        return np.asarray(out_v, np.float32), np.asarray(nf, np.int32)
+    v2, f2 = split(v, f)
+    if vt is None:
+        return v2, f2
+    vt2, ft2 = split(vt, ft)
+    return v2, f2, vt2, ft2
+
+
+def median_step(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def kernels_ms(fn, n=5):
+    """Per-kernel HIP-event durations recorded by the library (nr_profile_*), averaged over n steps."""
+    import ctypes
+    from neural_renderer_v2_pytorch_amd import _lib
+    names = ["k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
+    L = _lib.lib()
+    _lib.check(L.nr_profile_enable(1), "nr_profile_enable")
+    acc = {k: [] for k in names}
+    try:
+        for _ in range(n):
+            fn()
+            torch.cuda.synchronize()
+            for k in names:
+                ms = ctypes.c_float()
+                if L.nr_profile_read(k.encode(), ctypes.byref(ms)) == 0:
+                    acc[k].append(ms.value)
+    finally:
+        L.nr_profile_enable(0)
+    return {k: round(float(np.mean(v)), 5) for k, v in acc.items() if v}
+
+
+def scene(v, f, B, dev, seed=0):
+    vb = torch.as_tensor(synthetic.jittered(v, B, seed_base=1000 + seed))
+    eyes = torch.as_tensor(synthetic.viewpoints(B, seed_base=2000 + seed))
+    return synthetic.project(vb.to(dev), eyes.to(dev)).contiguous().detach().requires_grad_(True)
+
+
+def cfg2(dev, a):
+    v, f = nr.load_obj(os.path.join(DATA, "teapot.obj"))
+    B, s = 4, 256
+    proj = scene(v, f, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.as_tensor(np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32), device=dev)
+    tex.requires_grad_(True)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+    faces = torch.as_tensor(f, device=dev)
+    g = torch.randn((B, 5, s, s), device=dev)
+
+    def step():
+        proj.grad = tex.grad = None
+        nr.rasterize_core(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
+    t = median_step(step, a.steps, a.warmup)
+    return dict(config="cfg2 teapot B=4 256^2 rgb+sil+depth", faces=int(f.shape[0]), batch=B, image_size=s,
+                ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
+                kernels_ms=kernels_ms(step))
+
+
+def cfg3(dev, a):
+    v, f, vt, ft, tex = nr.load_obj(os.path.join(DATA, "4e49873292196f02574b5684eaec43e9", "model.obj"),
+                                    load_textures=True)
+    v, f, vt, ft = subdivide(v, f, vt, ft)
+    B, s = 64, 256
+    proj = scene(v, f, B, dev)
+    tex = torch.as_tensor(np.ascontiguousarray(tex), device=dev).float()
+    if tex.shape[0] != 3:
+        tex = tex.permute(2, 0, 1).contiguous()
+    tex.requires_grad_(True)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+    faces = torch.as_tensor(f, device=dev)
+    g = torch.randn((B, 4, s, s), device=dev)
+
+    def step():
+        proj.grad = tex.grad = None
+        nr.rasterize_rgba(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
+    t = median_step(step, a.steps, a.warmup)
+    return dict(config="cfg3 car (1x subdivided) B=64 256^2 textured rgba", faces=int(f.shape[0]), batch=B,
+                image_size=s, ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
+                kernels_ms=kernels_ms(step))
+
+
+def cfg5(dev, a):
+    v, f = synthetic.torus(250, 100)
+    s = 512
+    faces = torch.as_tensor(f, device=dev)
+    ren = nr.Renderer()
+    ren.image_size = s
+    ren.viewpoints = nr.get_points_from_angles(2.732, 30, -15)
+    with torch.no_grad():
+        target = ren.render_silhouettes(torch.as_tensor(v[None] * 1.1, device=dev), faces)
+    verts = torch.nn.Parameter(torch.as_tensor(v[None], device=dev))
+    opt = torch.optim.Adam([verts], lr=0.001)
+
+    def step():
+        opt.zero_grad()
+        loss = ((ren.render_silhouettes(verts, faces) - target) ** 2).sum()
+        loss.backward()
+        opt.step()
+    t = median_step(step, a.steps, a.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.loop_steps):
+        step()
+    torch.cuda.synchronize()
+    loop = time.perf_counter() - t0
+    return dict(config="cfg5 torus 50k faces, 512^2 (1024^2 internal) silhouettes, Renderer + Adam loop",
+                faces=int(f.shape[0]), batch=1, image_size=s, ms_per_step=round(t * 1e3, 4),
+                mpx_per_s=round(s * s / t / 1e6, 1), loop_steps=a.loop_steps, loop_s=round(loop, 4),
+                kernels_ms=kernels_ms(step))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--loop-steps", type=int, default=200)
+    p.add_argument("--only", default="cfg2,cfg3,cfg5")
+    a = p.parse_args()
+    dev = torch.device("cuda", 0)
+    for name in a.only.split(","):
+        r = globals()[name](dev, a)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1227,7 +1227,8 @@ template <bool LIT> constexpr int bwd_lds() {
 static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 // experiment switch for timing builds (never set in the shipped library):
 //   2 = no gradient accumulation (steps 3 and 4), 4 = no global atomics (step 4),
-//   8 = no per-face gather (step 3's member loop), 16 = no halo shading, 64 = no stencil
+//   8 = no per-face gather (step 3's member loop), 16 = no halo shading, 64 = no stencil,
+//   1024 = no direct texel atomics (texels outside a face's window)
 #ifndef NR_ABLATE
 #define NR_ABLATE 0
 #endif
@@ -1518,7 +1519,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
 #pragma unroll
                         for (int ch = 0; ch < 3; ch++) {
                             const float v = Gt[ch] * s.wt[i];
-                            if (v != 0.f) unsafeAtomicAdd(gtg + ch, v);
+                            if (v != 0.f && !(NR_ABLATE & 1024)) unsafeAtomicAdd(gtg + ch, v);
                         }
                     }
                 }
@@ -1703,6 +1704,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
     float* __restrict__ gNb = LIT ? a.grad_normals + (long long)b * a.F * 9 : nullptr;
     const bool act0 = P[0].fi >= 0, act1 = P[1].fi >= 0;
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
+    // texel lanes: consecutive faces with the same texel window (e.g. every face of a flat-colour
+    // material samples one 2x2 atlas patch, load_obj.py:84-94) accumulate into `pend` and flush once
+    // per run, so such hot texels take one atomic per run instead of one per face
+    float pend = 0.f;
+    int pwx = INT_MIN, pwy = 0;
     while (p0 | p1) {
         // leader: lowest pending pixel; both candidates read without branches, selected on the scalar unit
         const bool from0 = p0 != 0ull;
@@ -1760,13 +1766,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
         if (NR_ABLATE & 4) {
             asm volatile("" ::"v"(v));
         } else {
-            // one atomic per lane, address selected without branches
-            const int x = wx + tdx, y = wy + tdy;
-            const bool tex_lane = want_tex && chunk < 3 && wx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
+            // one atomic per lane, address selected without branches: face lanes add this face's
+            // floats; texel lanes flush the pending window when the window changes
+            const bool win = wx != INT_MIN;
+            const bool sw = win && (wx != pwx || wy != pwy);
+            const int x = pwx + tdx, y = pwy + tdy;
+            const bool tex_lane = want_tex && chunk < 3 && sw && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
             const bool face_lane = chunk == 3 && tt < 9;
+            const float fv = face_lane ? v : pend;
             float* dst = tex_lane ? g4b + (y * sh.tv.W + x) * 4 + chunk : gFb + key * 9 + tt;
-            if ((tex_lane || face_lane) && v != 0.f) unsafeAtomicAdd(dst, v);
+            if ((tex_lane || face_lane) && fv != 0.f) unsafeAtomicAdd(dst, fv);
+            if (win) {
+                pend = sw ? v : pend + v;
+                pwx = wx;
+                pwy = wy;
+            }
         }
+    }
+    if (!(NR_ABLATE & 4)) {  // the last pending window
+        const int x = pwx + tdx, y = pwy + tdy;
+        if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
+            unsafeAtomicAdd(g4b + (y * sh.tv.W + x) * 4 + chunk, pend);
     }
 }
 

@@ -8,6 +8,8 @@
 
 One step = rasterize_core forward + backward (cfg5: plus the Adam step), inputs resident on the GPU,
 median of the per-step times over --steps steps after --warmup.  Prints one JSON line per config.
+cfg2 is also timed as a HIP-graph replay of the captured step (graph_ms_per_step): at B=4 the eager
+step is bound by host launch overhead, not by the kernels.
 cfg1 is the reference's CPU-only plumbing case and cfg4 is bench.py --gpus 8.
 
 usage: python tools/bench_configs.py [--steps 20] [--warmup 5] [--loop-steps 200]
@@ -85,6 +87,21 @@ def kernels_ms(fn, n=5):
     return {k: round(float(np.mean(v)), 5) for k, v in acc.items() if v}
 
 
+def graphed(step):
+    """Capture one step in a HIP graph (torch.cuda.CUDAGraph) after a warm-up on a side stream and
+    return its replay: the launch-bound small-batch steps then cost their kernels only."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    return graph.replay
+
+
 def scene(v, f, B, dev, seed=0):
     vb = torch.as_tensor(synthetic.jittered(v, B, seed_base=1000 + seed))
     eyes = torch.as_tensor(synthetic.viewpoints(B, seed_base=2000 + seed))
@@ -98,18 +115,24 @@ def cfg2(dev, a):
     vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
     tex = torch.as_tensor(np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32), device=dev)
     tex.requires_grad_(True)
-    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
-                               faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+    vt_d, ft_d = torch.as_tensor(vt, device=dev), torch.as_tensor(ft, device=dev)
     faces = torch.as_tensor(f, device=dev)
     g = torch.randn((B, 5, s, s), device=dev)
 
     def step():
         proj.grad = tex.grad = None
+        # params (the expand of the leaf texture) built per step: graph-capture safe (see graphed)
+        params = nr.RasterizeParam(vertices_textures=vt_d[None].expand(B, -1, -1), faces_textures=ft_d,
+                                   textures=tex[None].expand(B, -1, -1, -1))
         nr.rasterize_core(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
     t = median_step(step, a.steps, a.warmup)
-    return dict(config="cfg2 teapot B=4 256^2 rgb+sil+depth", faces=int(f.shape[0]), batch=B, image_size=s,
-                ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
-                kernels_ms=kernels_ms(step))
+    res = dict(config="cfg2 teapot B=4 256^2 rgb+sil+depth", faces=int(f.shape[0]), batch=B, image_size=s,
+               ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
+               kernels_ms=kernels_ms(step))
+    proj.grad = tex.grad = None
+    tg = median_step(graphed(step), a.steps, a.warmup)
+    res.update(graph_ms_per_step=round(tg * 1e3, 4), graph_mpx_per_s=round(B * s * s / tg / 1e6, 1))
+    return res
 
 
 def cfg3(dev, a):

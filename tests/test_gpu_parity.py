@@ -280,6 +280,40 @@ def test_face_index_large_vs_oracle(oracle_mod, dev, S, level, B):
     assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
 
 
+@pytest.mark.parametrize("S,F,seed", [(64, 1500, 0), (96, 3000, 1), (64, 400, 2)])
+def test_face_index_dense_snapped_soup(oracle_mod, dev, S, F, seed):
+    """Deep bins (tens of faces over every 8x8 block, so k_raster_fwd's edge cull runs) of triangles
+    whose vertices sit exactly on pixel centres, many with an axis-aligned edge 1-2: along that
+    edge's line the reference's c2 is exactly 0, so its edge tests (.cu:107-116) pass pixels outside
+    the triangle, which may then win the z-test.  Bit-exact against the brute-force oracle, through
+    both the fused path's setup (vertices) and the caller-gathered entry point."""
+    r = np.random.RandomState(seed)
+    B = 2
+    centres = ((2 * np.arange(S) + 1 - S) / S).astype(np.float32)
+    ix = r.randint(0, S, size=(B, F, 3))
+    iy = r.randint(0, S, size=(B, F, 3))
+    flat = r.rand(B, F) < 0.5
+    iy[:, :, 2] = np.where(flat, iy[:, :, 1], iy[:, :, 2])           # edge 1-2 horizontal
+    ix[:, :, 2] = np.where(~flat & (r.rand(B, F) < 0.5), ix[:, :, 1], ix[:, :, 2])  # or vertical
+    # small triangles: the other corners within 6 pixels of corner 0
+    ix[:, :, 1:] = np.clip(ix[:, :, :1] + (ix[:, :, 1:] % 13) - 6, 0, S - 1)
+    iy[:, :, 1:] = np.clip(iy[:, :, :1] + (iy[:, :, 1:] % 13) - 6, 0, S - 1)
+    if True:  # keep the horizontal / vertical edges after the clipping
+        iy[:, :, 2] = np.where(flat, iy[:, :, 1], iy[:, :, 2])
+    z = r.uniform(0.5, 5.0, size=(B, F, 3)).astype(np.float32)
+    fg = np.stack([centres[ix], centres[iy], z], -1).astype(np.float32)  # [B, F, 3, 3]
+    ref = oracle_mod.face_index_map(torch.as_tensor(fg), S)
+    fim = nrr.compute_face_index_map(torch.as_tensor(fg, device=dev), nr.RasterizeHyperparam(image_size=S))
+    assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
+    # fused path: the same faces as a vertex list
+    verts = torch.as_tensor(fg.reshape(B, F * 3, 3), device=dev)
+    faces = torch.arange(F * 3, dtype=torch.int32, device=dev).reshape(F, 3)
+    hp = nr.RasterizeHyperparam(image_size=S, anti_aliasing=False)
+    hp.draw_rgb = False
+    _, fim2 = nrr.rasterize_core(verts, faces, nr.RasterizeParam(), hp, return_face_index=True)
+    assert np.array_equal(fim2.cpu().numpy(), ref), int((fim2.cpu().numpy() != ref).sum())
+
+
 def test_headline_properties(dev):
     """Full headline config (B=64, 256^2 AA, ico 5120, rgb+sil+depth): size-independent properties."""
     B = 64

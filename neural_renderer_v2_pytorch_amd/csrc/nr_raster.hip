@@ -1090,6 +1090,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
 
 // ------------------------------------------------------------------------------------------------
 // compute_weight_map (standalone entry point): one thread per pixel
+// k_shade_px: the same as k_shade with one thread per INTERNAL pixel.  k_shade's thread shades its
+// 2x2 quad in turn, each pixel a chain of three dependent loads (face-index map -> face / uv records
+// -> texels), so a wave waits on 12 serialised load latencies; here the four pixels of an output
+// pixel are four lanes of a DPP quad (lane q of the quad: q = 0 a=(iy+1,ix+1), 1 b=(iy,ix+1),
+// 2 c=(iy+1,ix), 3 d=(iy,ix)), their chains run concurrently, and the 2x2 mean is summed with
+// quad_perm broadcasts in the reference's order ((a + b) + c) + d (rasterize.py:321-328).  A block
+// covers 64 consecutive output pixels of one output row.  Without anti-aliasing a thread is one
+// output pixel.  Every internal pixel on a backward tile border stores itself to the halo cache.
+// Measured: k_shade_px is faster only when the grid is small (teapot B=4: 0.0176 -> 0.0136 ms); on the
+// headline the 2x2-per-thread k_shade wins (0.121 vs 0.164 ms: shading is VALU-bound there, and the
+// per-pixel form repeats the per-thread overheads 4x).  NR_SHADE_PX: 0 never, 1 always, 2 by grid size.
+#ifndef NR_SHADE_PX
+#define NR_SHADE_PX 2
+#endif
+template <int FEAT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 1 : 8, 8))) void k_shade_px(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
+                                                  int F, int S, Shade sh_in, int aa, float* __restrict__ images,
+                                                  float* __restrict__ halo) {
+    Shade sh = sh_in;
+    if (!(FEAT & 1)) sh.nl = 0;
+    if (!(FEAT & 2)) sh.bg = nullptr;
+    const int s = aa ? S / 2 : S;
+    const int b = blockIdx.y;
+    const int t = threadIdx.x;
+    const float* frb = face_records + (long long)b * F * FACE_REC;
+    const int32_t* fb = fim + (long long)b * S * S;
+    int o, x, y;
+    if (aa) {
+        o = blockIdx.x * 64 + (t >> 2);  // output pixel of this quad
+        const int q = t & 3;
+        const int oo = min(o, s * s - 1);
+        const int oi = oo / s, oj = oo - oi * s;
+        const int iy = S - 2 - 2 * oi, ix = S - 2 - 2 * oj;
+        y = iy + ((q & 1) ? 0 : 1);
+        x = ix + ((q & 2) ? 0 : 1);
+    } else {
+        o = blockIdx.x * 256 + t;
+        const int oo = min(o, s * s - 1);
+        const int oi = oo / s, oj = oo - oi * s;
+        y = S - 1 - oi;
+        x = S - 1 - oj;
+    }
+    const int fi = fb[y * S + x];
+    Face f = empty_face();
+    if (fi >= 0) f = load_face_rec(frb + fi * FACE_REC);
+    float v[MAXC];
+    shade_pixel(sh, b, fi, f, x, y, S, v);
+    const bool live = o < s * s;
+    if (halo && live) halo_store(halo, b, sh.C, S, x, y, v);
+    float* ob = images + (long long)b * sh.C * s * s + o;
+    if (!aa) {
+#pragma unroll
+        for (int c = 0; c < MAXC; c++)
+            if (c < sh.C && live) ob[c * s * s] = v[c];
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < MAXC; c++) {
+        if (c < sh.C) {
+            const int bits = __float_as_int(v[c]);
+            const float va = __int_as_float(__builtin_amdgcn_mov_dpp(bits, 0x00, 0xf, 0xf, false));
+            const float vb = __int_as_float(__builtin_amdgcn_mov_dpp(bits, 0x55, 0xf, 0xf, false));
+            const float vc = __int_as_float(__builtin_amdgcn_mov_dpp(bits, 0xaa, 0xf, 0xf, false));
+            const float vd = __int_as_float(__builtin_amdgcn_mov_dpp(bits, 0xff, 0xf, 0xf, false));
+            if ((t & 3) == 0 && live) ob[c * s * s] = (((va + vb) + vc) + vd) / 4.f;
+        }
+    }
+}
+
 __global__ void k_weight_map(const float* __restrict__ faces, const int32_t* __restrict__ fim, float* __restrict__ wm,
                              int F, int S, long long n) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2382,6 +2451,16 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     {
         ProfScope _p(P_SHADE, st);
         const Shade sh = make_shade(ra);
+        if (NR_SHADE_PX == 1 || (NR_SHADE_PX == 2 && ((long long)s * s + 255) / 256 * B < 4096)) {
+            const dim3 grid((unsigned)(((long long)s * s + (ra->anti_aliasing ? 63 : 255)) / (ra->anti_aliasing ? 64 : 256)), B);
+            switch ((sh.nl ? 1 : 0) | (sh.bg ? 2 : 0)) {
+                case 0: hipLaunchKernelGGL(k_shade_px<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+                case 1: hipLaunchKernelGGL(k_shade_px<1>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+                case 2: hipLaunchKernelGGL(k_shade_px<2>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+                default: hipLaunchKernelGGL(k_shade_px<3>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            }
+            return check_launch("k_shade");
+        }
         const dim3 grid((unsigned)(((long long)s * s + 255) / 256), B);
         switch ((sh.nl ? 1 : 0) | (sh.bg ? 2 : 0)) {
             case 0: hipLaunchKernelGGL(k_shade<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;

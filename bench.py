@@ -237,15 +237,16 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     ceiling = copy_ceiling_gbs(dev)
 
-    traffic = None
+    traffic = valu_busy = None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))
             if rec.get("config") == [args.batch, args.image_size, args.level, args.mode]:
                 traffic = rec.get("hbm_bytes_per_launch", {}).get(dominant)
+                valu_busy = rec.get("valu_busy", {}).get(dominant)
         except Exception:
-            traffic = None
+            traffic = valu_busy = None
 
     res = {
         "metric": "rasterize Mpixels/s fwd+bwd, 256² batch=64; % HBM roofline at 1 & 8 GPU",
@@ -268,7 +269,10 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5),
-                     "copy_ceiling_gbs": round(ceiling, 1)},
+                     "copy_ceiling_gbs": round(ceiling, 1),
+                     # the kernel's VALU issue share (PMC pass, tools/pmc_traffic.sh): with the HBM
+                     # share this shows the kernel is bound by neither -- latency
+                     "valu_busy": None if valu_busy is None else round(valu_busy, 3)},
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "step_roofline_frac": round(total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
     }

@@ -59,6 +59,49 @@ def optimize(model, iters, frames_dir=None):
     return losses
 
 
+def optimize_graphed(model, iters):
+    """optimize() with the whole step -- camera, rasterize, loss, backward, Adam -- captured once in a
+    HIP graph (torch.cuda.CUDAGraph) and replayed: the same kernels without the per-launch host
+    cost.  The viewpoint is held as a device tensor and Adam runs with capturable=True, so nothing
+    in the step touches the host; returns the loss of every step."""
+    dev = model.vertices.device
+    model.renderer.viewpoints = torch.as_tensor(
+        nr.get_points_from_angles(CAMERA_DISTANCE, ELEVATION, AZIMUTH), dtype=torch.float32, device=dev)
+    opt = torch.optim.Adam(model.parameters(), capturable=True)
+
+    def step():
+        loss = torch.sum((model.renderer.render_silhouettes(model.vertices, model.faces) - model.image_ref[None]) ** 2)
+        loss.backward()
+        opt.step()
+        return loss
+
+    # warm-up on a side stream (state allocation, cached faces checks), then capture one step
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    snapshot = model.vertices.detach().clone()
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    # undo the warm-up updates: the replays start from the initial mesh and a fresh Adam state
+    with torch.no_grad():
+        model.vertices.copy_(snapshot)
+        for st in opt.state.values():
+            for k, v in st.items():
+                if torch.is_tensor(v):
+                    v.zero_()
+    opt.zero_grad(set_to_none=True)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_loss = step()
+    losses = torch.empty(iters, device=dev)
+    for i in range(iters):
+        graph.replay()
+        losses[i] = static_loss
+    return losses.tolist()
+
+
 def save_frame(image, path):
     from PIL import Image
     a = image.cpu().numpy()
@@ -74,11 +117,12 @@ def main():
     ap.add_argument('--iters', type=int, default=300)
     ap.add_argument('--frames', default=None, help='directory for per-step frames (and the GIFs)')
     ap.add_argument('--gpu', type=int, default=0)
+    ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (no frames)')
     args = ap.parse_args()
     model = SilhouetteFit(args.obj, args.ref, torch.device('cuda', args.gpu))
     if args.frames:
         os.makedirs(args.frames, exist_ok=True)
-    losses = optimize(model, args.iters, args.frames)
+    losses = optimize_graphed(model, args.iters) if args.graph else optimize(model, args.iters, args.frames)
     print('loss: first %.1f, last %.1f after %d steps' % (losses[0], losses[-1], len(losses)))
     if args.frames:
         make_gif(args.frames, os.path.join(args.frames, 'example2_opt.gif'))

@@ -641,6 +641,22 @@ def test_example2_silhouette_fit(dev):
     assert losses[-1] < 0.01 * losses[0]
 
 
+def test_example2_graphed_fit(dev):
+    """The same fit with the whole step (camera, rasterize, loss, backward, Adam) captured once in a
+    HIP graph and replayed (examples/example2.py optimize_graphed): it must converge as the eager
+    loop does, from the same initial loss."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(__file__), '..', 'examples', 'example2.py')
+    spec = importlib.util.spec_from_file_location('nr_example2g', path)
+    ex = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ex)
+    model = ex.SilhouetteFit(os.path.join(ex.DATA, 'teapot.obj'), os.path.join(ex.DATA, 'example2_ref.png'), dev)
+    losses = ex.optimize_graphed(model, 300)
+    assert all(np.isfinite(losses))
+    assert 5000 < losses[0] < 20000
+    assert losses[-1] < 0.01 * losses[0]
+
+
 @pytest.mark.parametrize("B,shared_v,eye_kind,persp", [(2, False, "items", True), (3, False, "items", True),
                                                         (4, True, "items", True), (2, False, "one", False),
                                                         (3, True, "one", True)])

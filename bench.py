@@ -110,12 +110,13 @@ def kernel_bytes(w, args):
         "k_raster_bwd": fim + img + frec + (24 * F + T + T if rgb else 0) + frec,
         "k_vertex_grad": frec + 4 * (V + 1) + 12 * F + 12 * V * B,
         "k_tex_out": 2 * T,
+        "k_tex_pack": T + (4 * T // 3 if rgb else 0),  # read the planes, write RGBA rows
     }
     total = B * (8 * S * S + 8 * C * s * s + 36 * V) + 24 * F + (2 * T if T else 0)
     return k, total
 
 
-KERNELS = ["k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
+KERNELS = ["k_tex_pack", "k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
 
 
 def time_kernels(w, n=10):

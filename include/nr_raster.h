@@ -138,6 +138,11 @@ typedef struct NrRasterArgs {
     const float* backgrounds;
     long long bg_stride_b, bg_stride_c, bg_stride_y;
     float* grad_backgrounds;         /* backward output [B, 3, S, S] contiguous, fully written; or NULL */
+    /* optional, only with NR_DRAW_RGB: nr_texture_packed_bytes() of scratch that the forward fills
+     * with the texels as RGBA rows [Bt, ceil4(H*W), 4] (Bt = tex_stride_b ? B : 1) and the forward and
+     * backward then sample (one 16-B load per bilinear corner); kept by the caller from the forward
+     * to the backward.  NULL = sample `textures` directly (same results). */
+    float* textures_packed;
 } NrRasterArgs;
 
 enum { NR_LIGHT_AMBIENT = 0, NR_LIGHT_DIRECTIONAL = 1, NR_LIGHT_SPECULAR = 2, NR_LIGHT_FLOATS = 8 };
@@ -147,6 +152,9 @@ NR_API int nr_num_channels(int draw_flags);
 
 /* rasterize.py:194-329 (without lights / backgrounds): images [B, C, s, s] contiguous. */
 NR_API int nr_rasterize_forward(const NrRasterArgs* args, float* images, void* stream);
+
+/* Bytes of NrRasterArgs.textures_packed for texture_items textures of H x W texels. */
+NR_API size_t nr_texture_packed_bytes(int texture_items, int tex_height, int tex_width);
 
 /* Bytes of NrRasterArgs.halo for B items at output size s (internal 2s with anti-aliasing). */
 NR_API size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw_flags);
@@ -213,7 +221,7 @@ NR_API int nr_selftest_division(const float* a, const float* b, float* q_fast, f
 /* Measurement hook (bench.py's roofline leg; no reference counterpart).  With profiling on, the
  * library brackets each launch of its kernels with a pair of HIP events recorded on the launch
  * stream; nr_profile_read gives the duration in ms of the most recent launch of `kernel`
- * ("k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out") once
+ * ("k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out", "k_tex_pack") once
  * the stream has been synchronised.  Process-wide state, meant for a single measuring thread. */
 NR_API int nr_profile_enable(int on);
 NR_API int nr_profile_read(const char* kernel, float* ms);

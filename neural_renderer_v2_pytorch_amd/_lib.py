@@ -24,7 +24,7 @@ EXPORTS = [
     "nr_differentiation_backward", "nr_num_channels", "nr_rasterize_forward", "nr_rasterize_backward",
     "nr_backward_workspace_bytes", "nr_profile_enable", "nr_profile_read",
     "nr_selftest_division", "nr_halo_bytes", "nr_raster_args_size", "nr_rasterize_backward_params",
-    "nr_camera_forward", "nr_camera_backward", "nr_camera_workspace_bytes",
+    "nr_camera_forward", "nr_camera_backward", "nr_camera_workspace_bytes", "nr_texture_packed_bytes",
 ]
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
@@ -46,7 +46,7 @@ class NrRasterArgs(ctypes.Structure):
         ("num_lights", c_int), ("lights", c_void_p), ("face_normals", c_void_p), ("vertex_normals", c_void_p),
         ("normal_offsets", c_void_p), ("normal_faces", c_void_p),
         ("backgrounds", c_void_p), ("bg_stride_b", c_ll), ("bg_stride_c", c_ll), ("bg_stride_y", c_ll),
-        ("grad_backgrounds", c_void_p),
+        ("grad_backgrounds", c_void_p), ("textures_packed", c_void_p),
     ]
 
 NR_LIGHT_AMBIENT, NR_LIGHT_DIRECTIONAL, NR_LIGHT_SPECULAR, NR_LIGHT_FLOATS = 0, 1, 2, 8
@@ -92,6 +92,8 @@ def lib():
     L.nr_camera_forward.argtypes = [ctypes.POINTER(NrCameraArgs), c_void_p, c_void_p]
     L.nr_camera_backward.argtypes = [ctypes.POINTER(NrCameraArgs), c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                      c_void_p]
+    L.nr_texture_packed_bytes.restype = c_size_t
+    L.nr_texture_packed_bytes.argtypes = [c_int, c_int, c_int]
     L.nr_camera_workspace_bytes.restype = c_size_t
     L.nr_camera_workspace_bytes.argtypes = [c_int]
     L.nr_backward_workspace_bytes.restype = c_size_t
@@ -105,7 +107,8 @@ def lib():
     L.nr_profile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(c_float)]
     for name in EXPORTS:
         if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels", "nr_backward_workspace_bytes",
-                        "nr_halo_bytes", "nr_raster_args_size", "nr_camera_workspace_bytes"):
+                        "nr_halo_bytes", "nr_raster_args_size", "nr_camera_workspace_bytes",
+                        "nr_texture_packed_bytes"):
             getattr(L, name).restype = c_int
     _lib = L
     return L

@@ -68,9 +68,9 @@ int check_launch(const char* what) {
 }
 
 // ---- measurement hook (nr_profile_enable / nr_profile_read) ----
-enum { P_SETUP, P_RASTER, P_SHADE, P_BWD, P_VGRAD, P_TEXOUT, P_N };
+enum { P_SETUP, P_RASTER, P_SHADE, P_BWD, P_VGRAD, P_TEXOUT, P_TEXPACK, P_N };
 const char* const kProfNames[P_N] = {"k_face_setup", "k_raster_fwd", "k_shade",
-                                     "k_raster_bwd", "k_vertex_grad", "k_tex_out"};
+                                     "k_raster_bwd", "k_vertex_grad", "k_tex_out", "k_tex_pack"};
 bool g_prof = false;
 hipEvent_t g_prof_ev[P_N][2];
 bool g_prof_rec[P_N];
@@ -248,6 +248,10 @@ struct TexView {
     long long sb;   // item stride (uniform 64-bit part)
     int sc, sp;     // channel / texel strides: one item's view spans < 2^31 elements (validate_raster)
     int H, W;
+    // the same texels packed as RGBA rows [Bt][HWp] (NrRasterArgs.textures_packed), or null: one 16-B
+    // load per bilinear corner, and 2 cache lines per pixel instead of 6 (3 channel planes x 2 rows)
+    const float4* __restrict__ t4;
+    int HWp;
 };
 
 __device__ __forceinline__ float texel(const TexView& t, int b, int c, int p) {
@@ -323,12 +327,27 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
     s.wt[3] = (s.y - s.y0) * (s.x - s.x0);
     const float* tb = tv.tex + (long long)bt * tv.sb;
     int off[4];
+    float4 q4[4];
+    if (tv.t4) {
+        const float4* t4b = tv.t4 + (long long)bt * tv.HWp;
 #pragma unroll
-    for (int i = 0; i < 4; i++) off[i] = s.idx[i] * tv.sp;
+        for (int i = 0; i < 4; i++) q4[i] = t4b[s.idx[i]];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) off[i] = s.idx[i] * tv.sp;
+    }
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         const float* tc = tb + c * tv.sc;
-        const float t0 = tc[off[0]], t1 = tc[off[1]], t2 = tc[off[2]], t3 = tc[off[3]];
+        float t0, t1, t2, t3;
+        if (tv.t4) {
+            t0 = c == 0 ? q4[0].x : (c == 1 ? q4[0].y : q4[0].z);
+            t1 = c == 0 ? q4[1].x : (c == 1 ? q4[1].y : q4[1].z);
+            t2 = c == 0 ? q4[2].x : (c == 1 ? q4[2].y : q4[2].z);
+            t3 = c == 0 ? q4[3].x : (c == 1 ? q4[3].y : q4[3].z);
+        } else {
+            t0 = tc[off[0]], t1 = tc[off[1]], t2 = tc[off[2]], t3 = tc[off[3]];
+        }
         s.rgb[c] = ((s.wt[0] * t0 + s.wt[1] * t1) + s.wt[2] * t2) + s.wt[3] * t3;
         if (G) {
             if (c == 0) {
@@ -1012,7 +1031,7 @@ __device__ __forceinline__ void halo_store(float* __restrict__ halo, int b, int 
 // occupancy); costs one extra read of the face-index map.
 template <int FEAT>  // 1 = lights, 2 = backgrounds, as k_raster_bwd
 #ifndef NR_SHADE_WPE
-#define NR_SHADE_WPE 7  // 7 waves/SIMD: 68 VGPRs, no spills (the unlit instantiations)
+#define NR_SHADE_WPE 6  // 6 waves/SIMD: up to 80 VGPRs, no spills with the packed-texel path (7: a 2-dword spill, same time)
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 1 : NR_SHADE_WPE, 8))) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
                                                int F, int S, Shade sh_in, int aa, float* __restrict__ images,
@@ -2306,6 +2325,21 @@ __global__ void k_camera_eye(NrCameraArgs c, const float* __restrict__ acc, floa
     ge[t * 3 + 2] = tot[2];
 }
 
+// textures [Bt, 3, H, W] (any strides) -> RGBA rows [Bt, HWp, 4] (alpha slot 0), read by the sampling
+__global__ void k_tex_pack(const float* __restrict__ tex, long long sb, int sc, int sp, int HW, int HWp,
+                           float4* __restrict__ out, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const long long bt = i / HWp;
+    const int p = (int)(i - bt * HWp);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < HW) {
+        const float* tb = tex + bt * sb + (long long)p * sp;
+        v = make_float4(tb[0], tb[sc], tb[2 * (long long)sc], 0.f);
+    }
+    out[i] = v;
+}
+
 int validate_raster(const NrRasterArgs* a, bool need_workspace) {
     if (!a) return fail(NR_ERR_ARGS, "null args");
     if (a->batch_size < 0 || a->num_faces < 0 || a->num_vertices < 0 || a->image_size <= 0)
@@ -2347,6 +2381,8 @@ Shade make_shade(const NrRasterArgs* a) {
     sh.tv.sp = (int)a->tex_stride_p;
     sh.tv.H = a->tex_height;
     sh.tv.W = a->tex_width;
+    sh.tv.t4 = reinterpret_cast<const float4*>(a->textures_packed);
+    sh.tv.HWp = (a->tex_height * a->tex_width + 3) & ~3;
     sh.face_uv = a->face_uv;
     sh.uv_bstride = a->vt_batch_stride ? (long long)a->num_faces * 8 : 0;
     const bool rgb = (a->draw_flags & NR_DRAW_RGB) != 0;
@@ -2525,10 +2561,26 @@ int nr_rasterize_forward(const NrRasterArgs* a, float* images, void* stream) {
     int e = validate_raster(a, true);
     if (e) return e;
     if (!images && a->batch_size > 0) return fail(NR_ERR_ARGS, "null images");
+    if ((a->draw_flags & NR_DRAW_RGB) && a->textures_packed && a->batch_size > 0) {
+        const int tex_items = a->tex_stride_b ? a->batch_size : 1;
+        const int HW = a->tex_height * a->tex_width, HWp = (HW + 3) & ~3;
+        const long long n = (long long)tex_items * HWp;
+        ProfScope _p(P_TEXPACK, (hipStream_t)stream);
+        hipLaunchKernelGGL(k_tex_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a->textures,
+                           a->tex_stride_b, (int)a->tex_stride_c, (int)a->tex_stride_p, HW, HWp,
+                           reinterpret_cast<float4*>(a->textures_packed), n);
+        e = check_launch("k_tex_pack");
+        if (e) return e;
+    }
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
     return run_face_index(a->vertices, a->faces, a->face_records, a->face_index, a->batch_size, a->num_vertices,
                           a->num_faces, S, a->near, a->far, a->draw_backside, a->depth_min_delta, a->workspace,
                           a->workspace_bytes, (hipStream_t)stream, a, images);
+}
+
+size_t nr_texture_packed_bytes(int texture_items, int tex_height, int tex_width) {
+    if (texture_items <= 0 || tex_height <= 0 || tex_width <= 0) return 0;
+    return (size_t)texture_items * ((((size_t)tex_height * tex_width) + 3) & ~size_t(3)) * 16;
 }
 
 size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw_flags) {

@@ -223,7 +223,7 @@ class _Cfg:
 
 
 def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj=None, halo=None, light=None,
-          bg=None):
+          bg=None, tex4=None):
     a = _lib.NrRasterArgs()
     a.batch_size = cfg.B
     a.num_vertices = cfg.V
@@ -269,12 +269,17 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj
             a.backgrounds = bg[0].data_ptr()
             a.bg_stride_b, a.bg_stride_c, a.bg_stride_y = bg[0].stride(0), bg[0].stride(1), bg[0].stride(2)
             a.grad_backgrounds = bg[1].data_ptr() if bg[1] is not None else None
+        if tex4 is not None:  # RGBA-packed texels (NrRasterArgs.textures_packed)
+            a.textures_packed = tex4.data_ptr()
     return a
 
 
 # the forward stores the backward's tile-border image values (NrRasterArgs.halo); False makes the
 # backward re-shade its halos instead (same results; the parity tests cover both)
 _HALO_CACHE = os.environ.get("NR_HALO_CACHE", "1") != "0"
+# the forward packs the texels into RGBA rows that forward and backward sample (NrRasterArgs.
+# textures_packed); False samples the [B, 3, H, W] textures directly (same results)
+_TEX_PACK = os.environ.get("NR_TEX_PACK", "1") != "0"
 
 
 class Rasterize(torch.autograd.Function):
@@ -310,12 +315,18 @@ class Rasterize(torch.autograd.Function):
             light = (light_recs, torch.empty((B, cfg.F, 3), dtype=torch.float32, device=dev),
                      torch.empty((B, cfg.V, 4), dtype=torch.float32, device=dev), nadj[0], nadj[1])
         bg = (backgrounds, None) if backgrounds is not None else None
+        tex4 = None
+        if rgb and _TEX_PACK:
+            H, W = cfg.tex_hw
+            tex4 = torch.empty(L.nr_texture_packed_bytes(1 if cfg.tex_shared else B, H, W) // 4, dtype=torch.float32,
+                               device=dev)
         a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws,
-                  halo=halo, light=light, bg=bg)
+                  halo=halo, light=light, bg=bg, tex4=tex4)
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_forward(a, _lib.ptr(images), _lib.stream_of(vertices)), "nr_rasterize_forward")
         ctx.cfg = cfg
         ctx.light = light
+        ctx.tex4 = tex4
         ctx.save_for_backward(vertices, textures, vertices_textures, faces, faces_textures, face_records, face_uv,
                               fim, halo, backgrounds)
         ctx.mark_non_differentiable(fim)
@@ -352,7 +363,8 @@ class Rasterize(torch.autograd.Function):
         if backgrounds is not None and ctx.needs_input_grad[5]:
             gbg = torch.empty((cfg.B, 3) + tuple(backgrounds.shape[2:]), dtype=torch.float32, device=dev)
         bg = (backgrounds, gbg) if backgrounds is not None else None
-        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo, ctx.light, bg)
+        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo, ctx.light, bg,
+                  tex4=ctx.tex4)
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),
                                                ws.numel(), _lib.stream_of(vertices)), "nr_rasterize_backward")

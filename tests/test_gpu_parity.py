@@ -76,6 +76,17 @@ def test_textured_scene(golden, dev, name):
     close_grads(tex_leaf.grad, d["grad_textures"], name + " grad textures")
 
 
+@pytest.mark.parametrize("name", ["teapot_rgbsd_aa", "ico_rgbsd_aa"])
+def test_textured_scene_unpacked_textures(golden, dev, name):
+    """The same goldens with the texels sampled straight from the [B, 3, H, W] textures instead of
+    the forward's RGBA-packed copy (NrRasterArgs.textures_packed = NULL): both layouts are exact."""
+    try:
+        nrr._TEX_PACK = False
+        test_textured_scene(golden, dev, name)
+    finally:
+        nrr._TEX_PACK = True
+
+
 def test_wrappers_match_core(golden, dev):
     """rasterize_rgba / rasterize_rgb set the draw flags on the passed hyperparams (rasterize.py:341-356)."""
     d = golden("teapot_rgba_aa")

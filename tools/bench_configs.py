@@ -70,7 +70,7 @@ def kernels_ms(fn, n=5):
     """Per-kernel HIP-event durations recorded by the library (nr_profile_*), averaged over n steps."""
     import ctypes
     from neural_renderer_v2_pytorch_amd import _lib
-    names = ["k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
+    names = ["k_tex_pack", "k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
     L = _lib.lib()
     _lib.check(L.nr_profile_enable(1), "nr_profile_enable")
     acc = {k: [] for k in names}

@@ -280,6 +280,7 @@ _HALO_CACHE = os.environ.get("NR_HALO_CACHE", "1") != "0"
 # the forward packs the texels into RGBA rows that forward and backward sample (NrRasterArgs.
 # textures_packed); False samples the [B, 3, H, W] textures directly (same results)
 _TEX_PACK = os.environ.get("NR_TEX_PACK", "1") != "0"
+_TEX_PACK_MAX_BYTES = 1 << 31
 
 
 class Rasterize(torch.autograd.Function):
@@ -318,8 +319,9 @@ class Rasterize(torch.autograd.Function):
         tex4 = None
         if rgb and _TEX_PACK:
             H, W = cfg.tex_hw
-            tex4 = torch.empty(L.nr_texture_packed_bytes(1 if cfg.tex_shared else B, H, W) // 4, dtype=torch.float32,
-                               device=dev)
+            nbytes = L.nr_texture_packed_bytes(1 if cfg.tex_shared else B, H, W)
+            if nbytes <= _TEX_PACK_MAX_BYTES:  # per-item atlases of hundreds of MB are sampled in place
+                tex4 = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
         a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws,
                   halo=halo, light=light, bg=bg, tex4=tex4)
         with torch.cuda.device(dev):

@@ -225,11 +225,19 @@ def main():
     gather_ms = None
     if not args.no_gather and world > 1:
         out = torch.empty((world,) + tuple(images.shape), device=dev, dtype=images.dtype)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        torch.distributed.all_gather_into_tensor(out, images.detach().contiguous())
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - t1) * 1e3
+        src = images.detach().contiguous()
+        torch.distributed.all_gather_into_tensor(out, src)  # warm-up: RCCL sets up its channels lazily
+        times = []
+        for _ in range(3):
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            torch.distributed.all_gather_into_tensor(out, src)
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t1) * 1e3)
+        t = torch.tensor([min(times)], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        gather_ms = float(t.item())
 
     kms = time_kernels(w)
     kb, total_bytes = kernel_bytes(w, args)

@@ -596,7 +596,12 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
                                                     int uv_items, float* __restrict__ fnorm) {
     __shared__ int2 s_bb[SETUP_FACES];
-    __shared__ uint32_t s_mask[SETUP_LDS_WORDS];
+    // the block's face records, assembled per face and then written out coalesced (a record per lane
+    // would store 64-B strided rows); the bin-mask words reuse the space afterwards
+    constexpr int STAGE = SETUP_FACES * FACE_REC;
+    __shared__ __attribute__((aligned(16))) float s_stage[STAGE > SETUP_LDS_WORDS ? STAGE : SETUP_LDS_WORDS];
+    float* s_frec = s_stage;
+    uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_stage);
     const int b = blockIdx.y;
     const int f0 = blockIdx.x * SETUP_FACES;
     const int t = threadIdx.x;
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
 #else
                 const int flags = (fxyz ? FACE_FAST_XYZ : 0) | (fzq ? FACE_FAST_ZQ : 0);
 #endif
-                float4* rec = reinterpret_cast<float4*>(face_records + ((long long)b * F + f) * FACE_REC);
+                float4* rec = reinterpret_cast<float4*>(s_frec + t * FACE_REC);
                 rec[0] = make_float4(c[0], c[1], c[2], c[3]);
                 rec[1] = make_float4(c[4], c[5], c[6], c[7]);
                 rec[2] = make_float4(c[8], rcp_nr(c[2]), rcp_nr(c[5]), rcp_nr(c[8]));
@@ -682,6 +687,15 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         s_bb[t] = bb;
     }
     __syncthreads();
+    {
+        const int nf = min(SETUP_FACES, F - f0);
+        if (GATHER) {
+            float4* dst = reinterpret_cast<float4*>(face_records + ((long long)b * F + f0) * FACE_REC);
+            const float4* src = reinterpret_cast<const float4*>(s_frec);
+            for (int i = t; i < nf * (FACE_REC / 4); i += blockDim.x) dst[i] = src[i];
+        }
+        __syncthreads();
+    }
     // coarse-bin bitmask words of this face group
     const int w0 = blockIdx.x * (SETUP_FACES / 32);
     const int nw = min(SETUP_FACES / 32, nwords - w0);

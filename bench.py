@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--mode", choices=["rgbsd", "sil"], default="rgbsd")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="gloo: rehearse the N > 1 path with ranks sharing GPUs (not for reported numbers)")
     p.add_argument("--no-gather", action="store_true",
                    help="with N > 1, skip the RCCL all_gather of the images timed after the steps (cfg4)")
     return p.parse_args()
@@ -50,8 +52,15 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            # rehearsal of the multi-rank code path on a box with fewer GPUs than ranks: gloo, ranks
+            # sharing devices (never used for reported numbers)
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     return world, rank, torch.device("cuda", local if world > 1 else 0)
@@ -224,7 +233,7 @@ def main():
 
     gather_ms = None
     if not args.no_gather and world > 1:
-        out = torch.empty((world,) + tuple(images.shape), device=dev, dtype=images.dtype)
+        out = torch.empty((world * images.shape[0],) + tuple(images.shape[1:]), device=dev, dtype=images.dtype)
         src = images.detach().contiguous()
         torch.distributed.all_gather_into_tensor(out, src)  # warm-up: RCCL sets up its channels lazily
         times = []

@@ -583,6 +583,51 @@ __device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Texture repacking, carried by other launches: textures [Bt, 3, H, W] (any strides) -> RGBA rows
+// [Bt, HWp, 4] (alpha slot 0) before the sampling (k_face_setup's idle threads), and the [Bt, HWp, 4]
+// gradient accumulator -> [Bt, 3, H, W] after the backward (k_vertex_grad's blocks).  Each block of
+// the carrying grid takes one contiguous slice, so neither needs a launch of its own.
+struct TexPack {
+    const float* __restrict__ tex;
+    long long sb;
+    int sc, sp, HW, HWp;
+    float4* __restrict__ out;  // null: nothing to pack
+    long long n;               // Bt * HWp
+};
+struct TexOut {
+    const float* __restrict__ g4;
+    float* __restrict__ out;   // null: nothing to write
+    int HW, HWp;
+    long long n;               // Bt * HW
+};
+__device__ __forceinline__ void tex_pack_one(const TexPack& pk, long long i) {
+    const long long bt = i / pk.HWp;
+    const int p = (int)(i - bt * pk.HWp);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < pk.HW) {
+        const float* tb = pk.tex + bt * pk.sb + (long long)p * pk.sp;
+        v = make_float4(tb[0], tb[pk.sc], tb[2 * (long long)pk.sc], 0.f);
+    }
+    pk.out[i] = v;
+}
+__device__ __forceinline__ void tex_out_one(const TexOut& to, long long i) {
+    const long long bt = i / to.HW;
+    const int p = (int)(i % to.HW);
+    const float4 v = reinterpret_cast<const float4*>(to.g4)[bt * to.HWp + p];
+    to.out[(bt * 3 + 0) * to.HW + p] = v.x;
+    to.out[(bt * 3 + 1) * to.HW + p] = v.y;
+    to.out[(bt * 3 + 2) * to.HW + p] = v.z;
+}
+// this block's slice [lo, hi) of n items spread over the whole grid
+__device__ __forceinline__ void grid_slice(long long n, long long& lo, long long& hi) {
+    const long long nb = (long long)gridDim.x * gridDim.y;
+    const long long id = (long long)blockIdx.y * gridDim.x + blockIdx.x;
+    const long long chunk = (n + nb - 1) / nb;
+    lo = min(id * chunk, n);
+    hi = min(lo + chunk, n);
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_face_setup: per (face group of 128, item)
 //   GATHER: faces come from vertices[b, faces_idx[f, k]] (rasterize.py:232) and are written to
 //           face_records; otherwise face_records already holds the gathered faces (the
@@ -594,7 +639,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     uint32_t* __restrict__ mask, int nbx, int nbins, int nwords,
                                                     const float* __restrict__ vt, long long vt_bstride, int Vt,
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
-                                                    int uv_items, float* __restrict__ fnorm) {
+                                                    int uv_items, float* __restrict__ fnorm, TexPack pk) {
     __shared__ int2 s_bb[SETUP_FACES];
     // the block's face records, assembled per face and then written out coalesced (a record per lane
     // would store 64-B strided rows); the bin-mask words reuse the space afterwards
@@ -605,6 +650,11 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
     const int b = blockIdx.y;
     const int f0 = blockIdx.x * SETUP_FACES;
     const int t = threadIdx.x;
+    if (pk.out && t >= SETUP_FACES) {  // the threads the face phase leaves idle repack the textures
+        long long lo, hi;
+        grid_slice(pk.n, lo, hi);
+        for (long long i = lo + (t - SETUP_FACES); i < hi; i += blockDim.x - SETUP_FACES) tex_pack_one(pk, i);
+    }
     if (t < SETUP_FACES) {
         const int f = f0 + t;
         int2 bb = make_int2(NR_EMPTY_RANGE, NR_EMPTY_RANGE);
@@ -1895,7 +1945,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
 // gathered-face gradient -> vertex gradient: gV[b, v] = sum over (f, k) with faces[f, k] = v of gF[b, f, k]
 // (the index backward of rasterize.py:232), through a CSR adjacency built once per faces tensor.
 __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __restrict__ off,
-                              const int32_t* __restrict__ ent, float* __restrict__ gV, int F, int V, long long n) {
+                              const int32_t* __restrict__ ent, float* __restrict__ gV, int F, int V, long long n,
+                              TexOut to) {
+    if (to.out) {  // this block's slice of the texture-gradient transpose
+        long long lo, hi;
+        grid_slice(to.n, lo, hi);
+        for (long long j = lo + threadIdx.x; j < hi; j += blockDim.x) tex_out_one(to, j);
+    }
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int b = (int)(i / V), v = (int)(i % V);
@@ -1978,15 +2034,9 @@ __global__ void k_fnormal_bwd(const float* __restrict__ face_records, const int3
 }
 
 // [Bt, HWp, 4] accumulation layout -> [Bt, 3, H, W]
-__global__ void k_tex_out(const float* __restrict__ g4, float* __restrict__ out, int HW, int HWp, long long n) {
+__global__ void k_tex_out(TexOut to) {  // standalone form (no vertex gradient to carry it)
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const long long bt = i / HW;
-    const int p = (int)(i % HW);
-    const float4 v = reinterpret_cast<const float4*>(g4)[bt * HWp + p];
-    out[(bt * 3 + 0) * HW + p] = v.x;
-    out[(bt * 3 + 1) * HW + p] = v.y;
-    out[(bt * 3 + 2) * HW + p] = v.z;
+    if (i < to.n) tex_out_one(to, i);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2340,18 +2390,9 @@ __global__ void k_camera_eye(NrCameraArgs c, const float* __restrict__ acc, floa
 }
 
 // textures [Bt, 3, H, W] (any strides) -> RGBA rows [Bt, HWp, 4] (alpha slot 0), read by the sampling
-__global__ void k_tex_pack(const float* __restrict__ tex, long long sb, int sc, int sp, int HW, int HWp,
-                           float4* __restrict__ out, long long n) {
+__global__ void k_tex_pack(TexPack pk) {  // standalone form (no face setup to carry it)
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const long long bt = i / HWp;
-    const int p = (int)(i - bt * HWp);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p < HW) {
-        const float* tb = tex + bt * sb + (long long)p * sp;
-        v = make_float4(tb[0], tb[sc], tb[2 * (long long)sc], 0.f);
-    }
-    out[i] = v;
+    if (i < pk.n) tex_pack_one(pk, i);
 }
 
 int validate_raster(const NrRasterArgs* a, bool need_workspace) {
@@ -2445,11 +2486,22 @@ size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
 
 static int run_face_index(const float* vertices, const int32_t* faces_idx, float* face_records, int32_t* fim,
                           int B, int V, int F, int S, float near, float far, int draw_backside, float delta,
-                          void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images) {
+                          void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images,
+                          TexPack pk) {
     const Geom g = make_geom(F, S);
     int2* bbox = (int2*)ws;
     uint32_t* mask = (uint32_t*)((char*)ws + ws_bbox_bytes(B, F));
     if (B == 0) return NR_OK;
+    // the setup's idle threads repack the textures when that takes them a few texels each; with no
+    // setup launch, or a texture too large for that, the repacking gets a launch of its own
+    const long long setup_idle = (long long)((F + SETUP_FACES - 1) / SETUP_FACES) * B * (256 - SETUP_FACES);
+    if (pk.out && (F == 0 || pk.n > 8 * setup_idle)) {
+        ProfScope _p(P_TEXPACK, st);
+        hipLaunchKernelGGL(k_tex_pack, dim3((unsigned)((pk.n + 255) / 256)), dim3(256), 0, st, pk);
+        const int e = check_launch("k_tex_pack");
+        if (e) return e;
+        pk.out = nullptr;
+    }
     if (F > 0) {
         dim3 grid((F + SETUP_FACES - 1) / SETUP_FACES, B);
         const bool rgb = ra && (ra->draw_flags & NR_DRAW_RGB);
@@ -2461,11 +2513,11 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
-                               rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr);
+                               rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk);
         else
             hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), 0, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
-                               nullptr);
+                               nullptr, pk);
         int e = check_launch("k_face_setup");
         if (e) return e;
         if (lit && V > 0) {
@@ -2533,7 +2585,7 @@ int nr_face_index_map_forward_safe(const float* faces, int32_t* face_index, int 
         return fail(NR_ERR_WORKSPACE, "workspace too small");
     return run_face_index(nullptr, nullptr, const_cast<float*>(faces), face_index, batch_size, 0, num_faces,
                           image_size, near, far, draw_backside, depth_min_delta, workspace, workspace_bytes,
-                          (hipStream_t)stream, nullptr, nullptr);
+                          (hipStream_t)stream, nullptr, nullptr, TexPack{});
 }
 
 int nr_compute_weight_map(const float* faces, const int32_t* face_index_map, float* weight_map, int batch_size,
@@ -2575,21 +2627,22 @@ int nr_rasterize_forward(const NrRasterArgs* a, float* images, void* stream) {
     int e = validate_raster(a, true);
     if (e) return e;
     if (!images && a->batch_size > 0) return fail(NR_ERR_ARGS, "null images");
+    TexPack pk{};
     if ((a->draw_flags & NR_DRAW_RGB) && a->textures_packed && a->batch_size > 0) {
         const int tex_items = a->tex_stride_b ? a->batch_size : 1;
-        const int HW = a->tex_height * a->tex_width, HWp = (HW + 3) & ~3;
-        const long long n = (long long)tex_items * HWp;
-        ProfScope _p(P_TEXPACK, (hipStream_t)stream);
-        hipLaunchKernelGGL(k_tex_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a->textures,
-                           a->tex_stride_b, (int)a->tex_stride_c, (int)a->tex_stride_p, HW, HWp,
-                           reinterpret_cast<float4*>(a->textures_packed), n);
-        e = check_launch("k_tex_pack");
-        if (e) return e;
+        pk.tex = a->textures;
+        pk.sb = a->tex_stride_b;
+        pk.sc = (int)a->tex_stride_c;
+        pk.sp = (int)a->tex_stride_p;
+        pk.HW = a->tex_height * a->tex_width;
+        pk.HWp = (pk.HW + 3) & ~3;
+        pk.out = reinterpret_cast<float4*>(a->textures_packed);
+        pk.n = (long long)tex_items * pk.HWp;
     }
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
     return run_face_index(a->vertices, a->faces, a->face_records, a->face_index, a->batch_size, a->num_vertices,
                           a->num_faces, S, a->near, a->far, a->draw_backside, a->depth_min_delta, a->workspace,
-                          a->workspace_bytes, (hipStream_t)stream, a, images);
+                          a->workspace_bytes, (hipStream_t)stream, a, images, pk);
 }
 
 size_t nr_texture_packed_bytes(int texture_items, int tex_height, int tex_width) {
@@ -2685,20 +2738,31 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
             if (e) return e;
         }
     }
+    TexOut to{};
+    if (rgb) {
+        to.g4 = g4;
+        to.out = grad_textures;
+        to.HW = HW;
+        to.HWp = HWp;
+        to.n = (long long)tex_items * HW;
+    }
+    // k_vertex_grad's blocks also carry the texture-gradient transpose when that is a few texels per
+    // thread; otherwise (no vertices, or a large texture) it gets a launch of its own
+    const long long vgrad_threads = (nv + 255) / 256 * 256;
+    const bool carry = nv > 0 && to.n <= 8 * vgrad_threads;
     if (nv > 0) {
         {
             ProfScope _p(P_VGRAD, st);
             hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gF, a->vertex_offsets,
-                               a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv);
+                               a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv, carry ? to : TexOut{});
         }
         e = check_launch("k_vertex_grad");
         if (e) return e;
     }
-    if (rgb) {
-        const long long nt = (long long)tex_items * HW;
+    if (to.out && to.n > 0 && !carry) {
         {
             ProfScope _p(P_TEXOUT, st);
-            hipLaunchKernelGGL(k_tex_out, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, g4, grad_textures, HW, HWp, nt);
+            hipLaunchKernelGGL(k_tex_out, dim3((unsigned)((to.n + 255) / 256)), dim3(256), 0, st, to);
         }
         e = check_launch("k_tex_out");
     }

@@ -1475,8 +1475,12 @@ struct BwdPix {
 };
 
 // FEAT: 1 = lights, 2 = backgrounds (separate instantiations keep the plain path lean)
-template <int FEAT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : 4, 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
+// NPX: pixels per lane (2: 256 threads, a wave = 16x8 pixels; 1: 512 threads, a wave = 16x4 pixels)
+#ifndef NR_BWD_WPE1
+#define NR_BWD_WPE1 6
+#endif
+template <int FEAT, int NPX>
+__global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? NR_BWD_WPE1 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
     constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0;
     // features this instantiation does not have become compile-time constants (the shared
     // shade_pixel then carries no light / background code or arguments)
@@ -1508,7 +1512,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
     float* __restrict__ g4b = a.grad_tex4 ? a.grad_tex4 + (long long)bt * a.HWp * 4 : nullptr;
     // wave wid owns the 16x8 block at (16 (wid & 1), 8 (wid >> 1)); lane -> column lane & 15, rows lane >> 4 (+4)
     const int lx = (wid & 1) * 16 + (lane & 15);
-    const int ly0 = (wid >> 1) * 8 + (lane >> 4);
+    const int ly0 = (wid >> 1) * (4 * NPX) + (lane >> 4);
     const int px = tx0 + lx;
     const float xp = pix_center(px, S);
 
@@ -1549,10 +1553,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
 #endif
 
     // ---- 1. image + upstream gradient (LDS), and the stencil-independent gradient terms ---------
-    BwdPix P[2];
-    float I2[2][MAXC], G2[2][MAXC];
+    BwdPix P[NPX];
+    float I2[NPX][MAXC], G2[NPX][MAXC];
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < NPX; k++) {
         const int py = ty0 + ly0 + 4 * k;
         const bool inside = px < S && py < S;
         BwdPix& q = P[k];
@@ -1584,7 +1588,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
         }
     }
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < NPX; k++) {
         const int py = ty0 + ly0 + 4 * k;
         BwdPix& q = P[k];
         if (q.fi < 0) continue;
@@ -1731,7 +1735,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
         I2[k][4] = dep;
     }
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < NPX; k++) {
         const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
@@ -1785,9 +1789,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
     __syncthreads();
 
     // ---- 2. Differentiation.backward stencil -> coordinate-map gradient ------------------------
-    float gF[2][9];
+    float gF[NPX][9];
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < NPX; k++) {
         const BwdPix& q = P[k];
 #pragma unroll
         for (int j = 0; j < 9; j++) gF[k][j] = 0.f;
@@ -1821,7 +1825,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
     }
     if (NR_ABLATE & 2) {
 #pragma unroll
-        for (int k = 0; k < 2; k++)
+        for (int k = 0; k < NPX; k++)
 #pragma unroll
             for (int j = 0; j < 9; j++) asm volatile("" ::"v"(gF[k][j]));
         return;
@@ -1829,9 +1833,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
     __syncthreads();  // the staged records reuse the image / gradient LDS
 
     // ---- 3. stage this lane's two pixel records; group the wave's records by face --------------
-    float* rec = s_raw + wid * (128 * REC);
+    float* rec = s_raw + wid * (64 * NPX * REC);
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < NPX; k++) {
         float* r = rec + (k * 64 + lane) * REC;
         reinterpret_cast<float4*>(r)[0] = make_float4(P[k].ay, P[k].by, P[k].ax, P[k].bx);
         reinterpret_cast<float4*>(r)[1] = make_float4(__int_as_float(P[k].pos), P[k].grgb[0], P[k].grgb[1], P[k].grgb[2]);
@@ -1854,7 +1858,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
     const int fsel = 8 + (tt < 9 ? tt : 0);
     const int nsel_w = 20 + (tt < 9 ? tt / 3 : 0), nsel_n = 17 + (tt < 9 ? tt % 3 : 0);
     float* __restrict__ gNb = LIT ? a.grad_normals + (long long)b * a.F * 9 : nullptr;
-    const bool act0 = P[0].fi >= 0, act1 = P[1].fi >= 0;
+    // the second pixel's state (NPX == 1: none, never active)
+    const int fi1 = NPX > 1 ? P[NPX - 1].fi : -1, wx1 = NPX > 1 ? P[NPX - 1].wx : 0, wy1 = NPX > 1 ? P[NPX - 1].wy : 0;
+    const bool act0 = P[0].fi >= 0, act1 = fi1 >= 0;
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
     // texel lanes: consecutive faces with the same texel window (e.g. every face of a flat-colour
     // material samples one 2x2 atlas patch, load_obj.py:84-94) accumulate into `pend` and flush once
@@ -1865,13 +1871,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
         // leader: lowest pending pixel; both candidates read without branches, selected on the scalar unit
         const bool from0 = p0 != 0ull;
         const int l0 = from0 ? __builtin_ctzll(p0) : 0, l1 = p1 ? __builtin_ctzll(p1) : 0;
-        const int k0 = __builtin_amdgcn_readlane(P[0].fi, l0), k1 = __builtin_amdgcn_readlane(P[1].fi, l1);
-        const int x0w = __builtin_amdgcn_readlane(P[0].wx, l0), x1w = __builtin_amdgcn_readlane(P[1].wx, l1);
-        const int y0w = __builtin_amdgcn_readlane(P[0].wy, l0), y1w = __builtin_amdgcn_readlane(P[1].wy, l1);
+        const int k0 = __builtin_amdgcn_readlane(P[0].fi, l0), k1 = __builtin_amdgcn_readlane(fi1, l1);
+        const int x0w = __builtin_amdgcn_readlane(P[0].wx, l0), x1w = __builtin_amdgcn_readlane(wx1, l1);
+        const int y0w = __builtin_amdgcn_readlane(P[0].wy, l0), y1w = __builtin_amdgcn_readlane(wy1, l1);
         const int key = from0 ? k0 : k1, wx = from0 ? x0w : x1w, wy = from0 ? y0w : y1w;
         // key >= 0, so fi == key implies an active pixel
         const unsigned long long m0 = __builtin_amdgcn_ballot_w64(P[0].fi == key) & p0;
-        const unsigned long long m1 = __builtin_amdgcn_ballot_w64(P[1].fi == key) & p1;
+        const unsigned long long m1 = __builtin_amdgcn_ballot_w64(fi1 == key) & p1;
         p0 &= ~m0;
         p1 &= ~m1;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f, an = 0.f;
@@ -1940,6 +1946,23 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ?
         if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
             unsafeAtomicAdd(g4b + (y * sh.tv.W + x) * 4 + chunk, pend);
     }
+}
+
+// pixels per lane, per launch: 2 (256 threads) when the grid fills the chip many times over; 1 (512
+// threads, 6 waves/SIMD instead of 4) for small grids, where the waves, not the per-face work, are
+// short (teapot B=4: 0.041 -> 0.035 ms; torus 1024^2 B=1: 0.059 -> 0.048 ms; on the headline and the
+// car the smaller wave regions mean more face flushes: 0.405 -> 0.417 and 0.73 -> 0.84 ms).
+// NR_BWD_NPX: 0 by grid size, 1 / 2 forced (timing builds).
+#ifndef NR_BWD_NPX
+#define NR_BWD_NPX 0
+#endif
+template <int FEAT>
+void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
+    const bool one = NR_BWD_NPX == 1 || (NR_BWD_NPX == 0 && (long long)grid.x * grid.y < 8192);
+    if (one)
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
+    else
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
 }
 
 // gathered-face gradient -> vertex gradient: gV[b, v] = sum over (f, k) with faces[f, k] = v of gF[b, f, k]
@@ -2715,10 +2738,10 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
         ProfScope _p(P_BWD, st);
         const dim3 grid(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size);
         switch ((lit ? 1 : 0) | (sh.bg ? 2 : 0)) {
-            case 0: hipLaunchKernelGGL(k_raster_bwd<0>, grid, dim3(NT), 0, st, ba, g, sh); break;
-            case 1: hipLaunchKernelGGL(k_raster_bwd<1>, grid, dim3(NT), 0, st, ba, g, sh); break;
-            case 2: hipLaunchKernelGGL(k_raster_bwd<2>, grid, dim3(NT), 0, st, ba, g, sh); break;
-            default: hipLaunchKernelGGL(k_raster_bwd<3>, grid, dim3(NT), 0, st, ba, g, sh); break;
+            case 0: launch_bwd<0>(grid, st, ba, g, sh); break;
+            case 1: launch_bwd<1>(grid, st, ba, g, sh); break;
+            case 2: launch_bwd<2>(grid, st, ba, g, sh); break;
+            default: launch_bwd<3>(grid, st, ba, g, sh); break;
         }
     }
     e = check_launch("k_raster_bwd");

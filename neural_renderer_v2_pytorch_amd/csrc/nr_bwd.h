@@ -1,0 +1,877 @@
+// nr_bwd.h -- backward: k_raster_bwd, k_vertex_grad, normal backward, k_tex_out, k_param_bwd
+// Part of nr_raster.hip (one translation unit); see that file and DESIGN.md.
+#pragma once
+
+#pragma clang fp contract(off)
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// k_raster_bwd: one block per 32x16 pixels + 1-pixel halo; each wave owns a 16x8 block, 2 pixels per
+// lane.
+//   1. recompute the internal image I (all channels, bit-identical to the forward) and the upstream
+//      gradient G of the block + halo into LDS (Differentiation saved the images; the flip/AA
+//      backward is an index map and /4), and for the block's own pixels the gradient terms that do
+//      not depend on the stencil (depth and texture-coordinate paths to z, bilinear weights);
+//   2. the soft-gradient stencil (gx, gy) of Differentiation.backward, then the coordinate-map chain
+//      rule -> a 9-float gradient of the gathered face (rasterize.py:232);
+//   3. reduction without LDS float atomics (ds_add_f32 runs at ~3 cycles per lane on gfx950,
+//      tools/ubench_lds_atomics.hip): each lane stages its two pixel records in LDS; the wave groups
+//      its records by face (ballot match loop); for each face, lanes 0..47 own the 4x4 texel x RGB
+//      window of the face and lanes 48..56 its 9 gradient floats, and sum over the face's records;
+//   4. one global float atomic per lane and face: a whole face record and whole 4-texel RGBA rows,
+//      i.e. a handful of 64-byte requests per (face, wave).
+//   Texel contributions outside a face's 4x4 window (atlases with larger per-face texture regions)
+//   go straight to global atomics in step 1.
+constexpr int BH = 16;                        // block height
+constexpr int HW_ = TW + 2, HH_ = BH + 2, HN = HW_ * HH_;
+constexpr int NHALO = 2 * HW_ + 2 * BH;       // 100 halo pixels
+constexpr int TWIN = 4;                       // texel window edge per face
+// staged record: ay by ax bx | pos G_rgb[3] | gF[9] | pad (20 floats); with lights also dL/dnormal[3]
+// and the weights w[3] at 17..22 (24 floats)
+template <bool LIT> constexpr int srec() { return LIT ? 24 : 20; }
+constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
+constexpr int BWD_LDS_HALO = 2 * MAXC * 128 * 4;  // halo staging (step 0), after the I / G planes
+template <bool LIT> constexpr int bwd_lds() {
+#ifdef NR_BWD_LDS_SMALL
+    return BWD_LDS_IG + BWD_LDS_HALO;  // timing builds with NR_ABLATE & 2 only (no record staging)
+#endif
+    return BWD_LDS_IG + BWD_LDS_HALO > 4 * 128 * srec<LIT>() * 4 ? BWD_LDS_IG + BWD_LDS_HALO : 4 * 128 * srec<LIT>() * 4;
+}
+static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
+// experiment switch for timing builds (never set in the shipped library):
+//   2 = no gradient accumulation (steps 3 and 4), 4 = no global atomics (step 4),
+//   8 = no per-face gather (step 3's member loop), 16 = no halo shading, 64 = no stencil,
+//   1024 = no direct texel atomics (texels outside a face's window)
+#ifndef NR_ABLATE
+#define NR_ABLATE 0
+#endif
+#ifndef NR_HALO_EARLY
+#define NR_HALO_EARLY 1
+#endif
+
+struct BwdArgs {
+    const float* __restrict__ face_records;
+    const int32_t* __restrict__ fim;
+    const float* __restrict__ grad_images;
+    float* __restrict__ grad_faces;   // [B, F, 9]
+    float* __restrict__ grad_tex4;    // [Bt, HWp, 4] or null
+    const float* __restrict__ halo;   // halo cache written by the forward, or null (re-shade the halo)
+    float* __restrict__ grad_normals; // [B, F, 9] per-face corner vertex-normal gradients (lights)
+    float* __restrict__ grad_bg;      // [B, 3, S, S] or null
+    int F, aa, s, HWp;
+    float step, inv_step;
+    int step_pow2;                     // x / step == x * inv_step exactly
+};
+
+// upstream gradient of internal pixel (x, y): the flip / 2x2-mean backward is an index map and /4.
+// gi: this item's [C, s, s] upstream gradient (32-bit offsets inside it)
+__device__ __forceinline__ void upstream_grad(const BwdArgs& a, const float* __restrict__ gi, int C, int y, int x, int S,
+                                              float* G) {
+    if (a.aa) {
+        const int s = a.s;
+        const int o = ((S - 1 - y) >> 1) * s + ((S - 1 - x) >> 1);
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) G[c] = c < C ? gi[c * s * s + o] / 4.f : 0.f;
+    } else {
+        const int o = (S - 1 - y) * S + (S - 1 - x);
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) G[c] = c < C ? gi[c * S * S + o] : 0.f;
+    }
+}
+
+__device__ __forceinline__ float upstream_one(const BwdArgs& a, const float* __restrict__ gi, int y, int x, int S, int c) {
+    if (a.aa) {
+        const int s = a.s;
+        return gi[c * s * s + ((S - 1 - y) >> 1) * s + ((S - 1 - x) >> 1)] / 4.f;
+    }
+    return gi[c * S * S + (S - 1 - y) * S + (S - 1 - x)];
+}
+
+__device__ __forceinline__ float div_step(const BwdArgs& a, float x) { return a.step_pow2 ? x * a.inv_step : x / a.step; }
+
+__device__ __forceinline__ float stencil(const BwdArgs& a, const float* Im, const float* I0, const float* Ip,
+                                         const float* Gm, const float* G0, const float* Gp, int i, int n, int C) {
+    const bool has_p = i <= n - 2, has_m = i >= 1;
+    const float r_i = has_p ? div_step(a, -pair_dot(I0, Ip, Gp, C)) : 0.f;
+    const float r_m = has_m ? div_step(a, -pair_dot(Im, I0, G0, C)) : 0.f;
+    const float l_i = has_p ? div_step(a, -pair_dot(Ip, I0, G0, C)) : 0.f;
+    const float l_m = has_m ? div_step(a, -pair_dot(I0, Im, Gm, C)) : 0.f;
+    return pick_grad(r_i + r_m, l_m + l_i);
+}
+
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// position (hy, hx) in the (BH + 2) x (TW + 2) tile frame of halo pixel t < NHALO: top row, bottom
+// row, left column, right column
+__device__ __forceinline__ void halo_pixel(int t, int& hy, int& hx) {
+    if (t < HW_) { hy = 0; hx = t; }
+    else if (t < 2 * HW_) { hy = HH_ - 1; hx = t - HW_; }
+    else if (t < 2 * HW_ + BH) { hy = 1 + (t - 2 * HW_); hx = 0; }
+    else { hy = 1 + (t - 2 * HW_ - BH); hx = HW_ - 1; }
+}
+
+// Values (v0, v1, v2, v3) held by every lane; lane l ends with v_c summed over the four lanes
+// l & 15 + 16 k, where c = l >> 4.  v_permlane32_swap(A, B) leaves [A_lo | B_lo] and [A_hi | B_hi]
+// (32-lane halves), so their sum is A summed over the halves in the low half and B in the high
+// half; v_permlane16_swap does the same for 16-lane rows.
+__device__ __forceinline__ float chunk_reduce_scatter(float v0, float v1, float v2, float v3) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v2), false, false);
+    const float b0 = __uint_as_float(p[0]) + __uint_as_float(p[1]);  // rows 0,1: v0; rows 2,3: v2
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v1), __float_as_uint(v3), false, false);
+    const float b1 = __uint_as_float(q[0]) + __uint_as_float(q[1]);  // rows 0,1: v1; rows 2,3: v3
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(b0), __float_as_uint(b1), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);           // row c: v_c
+}
+
+// per interior pixel state carried across the stencil's barrier
+struct BwdPix {
+    int fi;            // face index (-1: background or outside)
+    float w[3];        // barycentric weights (compute_weight_map)
+    float gz[3];       // d/dz of the face corners through the depth and texture-coordinate paths
+    float grgb[3];     // upstream gradient of the rgb channels
+    float ay, by, ax, bx;
+    int pos;           // bilinear top-left texel relative to the face window: dx | dy << 8; -1 none
+    int wx, wy;        // face window origin (texels); INT_MIN when not windowed
+    float gn[3];       // lights: dL/d(smooth normal)
+};
+
+// FEAT: 1 = lights, 2 = backgrounds (separate instantiations keep the plain path lean)
+// NPX: pixels per lane (2: 256 threads, a wave = 16x8 pixels; 1: 512 threads, a wave = 16x4 pixels)
+#ifndef NR_BWD_WPE1
+#define NR_BWD_WPE1 6
+#endif
+template <int FEAT, int NPX>
+__global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? NR_BWD_WPE1 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
+    constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0;
+    // features this instantiation does not have become compile-time constants (the shared
+    // shade_pixel then carries no light / background code or arguments)
+    Shade sh = sh_in;
+    if (!LIT) sh.nl = 0;
+    if (!BG) sh.bg = nullptr;
+    constexpr int REC = srec<LIT>();
+    __shared__ __attribute__((aligned(16))) float s_raw[bwd_lds<LIT>() / 4];
+    float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
+    float(*s_G)[HN] = reinterpret_cast<float(*)[HN]>(s_raw + MAXC * HN);
+    const int b = blockIdx.y;
+    const int S = g.S;
+    const int C = sh.C;
+    const bool rgb = (sh.draw & NR_DRAW_RGB) != 0;
+    const bool want_tex = rgb && a.grad_tex4 != nullptr;
+    int tile_x, tile_y;
+    xcd_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(blockIdx.x, b, (S + TW - 1) / TW, (S + BH - 1) / BH, tile_x, tile_y);
+    const int tx0 = tile_x * TW;
+    const int ty0 = tile_y * BH;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wid = t >> 6;
+    const int bt = sh.tv.sb ? b : 0;
+    // per-item bases (uniform, 64-bit); per-pixel offsets below are 32-bit
+    const int32_t* __restrict__ fimb = a.fim + (long long)b * S * S;
+    const float* __restrict__ gimb = a.grad_images + (long long)b * C * (a.aa ? a.s * a.s : S * S);
+    const float* __restrict__ frb = a.face_records + (long long)b * a.F * FACE_REC;
+    const float* __restrict__ fuvb = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0);
+    float* __restrict__ gFb = a.grad_faces + (long long)b * a.F * 9;
+    float* __restrict__ g4b = a.grad_tex4 ? a.grad_tex4 + (long long)bt * a.HWp * 4 : nullptr;
+    // wave wid owns the 16x8 block at (16 (wid & 1), 8 (wid >> 1)); lane -> column lane & 15, rows lane >> 4 (+4)
+    const int lx = (wid & 1) * 16 + (lane & 15);
+    const int ly0 = (wid >> 1) * (4 * NPX) + (lane >> 4);
+    const int px = tx0 + lx;
+    const float xp = pix_center(px, S);
+
+    // halo ring from the forward's halo cache: asynchronous global -> LDS loads by waves 0 and 1
+    // (lane t < NHALO carries halo pixel t, ring order of halo_pixel), landed before the barrier
+    float(*s_hI)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4);
+    float(*s_hG)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4 + MAXC * 128);
+    auto halo_prefetch = [&]() {
+        if (a.halo && t < 128) {
+            int hy, hx;
+            halo_pixel(t, hy, hx);
+            const int hpy = ty0 - 1 + hy, hpx = tx0 - 1 + hx;
+            const bool h_in = t < NHALO && hpy >= 0 && hpy < S && hpx >= 0 && hpx < S;
+            int hoff = 0, hcs = 0;
+            if (h_in) halo_locate(C, S, hpx, hpy, hoff, hcs);
+            // opaque copies of the base pointers: keeps the compiler from sharing these address
+            // computations with step 1's (which would stretch their live ranges over it)
+            const float* hbase = a.halo;
+            const float* gbase = a.grad_images;
+            asm volatile("" : "+s"(hbase), "+s"(gbase));
+            const float* hsrc = hbase + b * halo_item_floats(S, C) + hoff;
+            const float* gsrc = gbase + (long long)b * C * (a.aa ? a.s * a.s : S * S);
+            if (h_in) gsrc += a.aa ? ((S - 1 - hpy) >> 1) * a.s + ((S - 1 - hpx) >> 1) : (S - 1 - hpy) * S + (S - 1 - hpx);
+            const int gplane = a.aa ? a.s * a.s : S * S;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                if (c < C) {
+                    __builtin_amdgcn_global_load_lds((const void*)(hsrc + c * hcs),
+                                                     (void __attribute__((address_space(3)))*)(&s_hI[c][wid * 64]), 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void*)(gsrc + c * gplane),
+                                                     (void __attribute__((address_space(3)))*)(&s_hG[c][wid * 64]), 4, 0, 0);
+                }
+            }
+        }
+    };
+#if NR_HALO_EARLY
+    halo_prefetch();  // in flight during step 1
+#endif
+
+    // ---- 1. image + upstream gradient (LDS), and the stencil-independent gradient terms ---------
+    BwdPix P[NPX];
+    float I2[NPX][MAXC], G2[NPX][MAXC];
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        const int py = ty0 + ly0 + 4 * k;
+        const bool inside = px < S && py < S;
+        BwdPix& q = P[k];
+        q.fi = inside ? fimb[py * S + px] : -1;
+        q.pos = -1;
+        q.wx = q.wy = INT_MIN;
+        q.w[0] = q.w[1] = q.w[2] = 0.f;
+        q.gz[0] = q.gz[1] = q.gz[2] = 0.f;
+        q.grgb[0] = q.grgb[1] = q.grgb[2] = 0.f;
+        q.ay = q.by = q.ax = q.bx = 0.f;
+        q.gn[0] = q.gn[1] = q.gn[2] = 0.f;
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) I2[k][c] = G2[k][c] = 0.f;
+        if (inside) upstream_grad(a, gimb, C, py, px, S, G2[k]);
+        if (BG && rgb && inside) {
+            // background pixels: rgb = 0 * 0 + 1 * bg (chainer rasterize.py:576); grad of bg = (1 - fg) G
+            const float fg = q.fi >= 0 ? 1.f : 0.f;
+            if (q.fi < 0) {
+                float bgc[3];
+                background(sh, b, px, py, S, bgc);
+#pragma unroll
+                for (int c = 0; c < 3; c++) I2[k][c] = fg * 0.f + (1.f - fg) * bgc[c];
+            }
+            if (a.grad_bg) {
+                float* gb = a.grad_bg + ((long long)b * 3) * S * S + (S - 1 - py) * S + (S - 1 - px);
+#pragma unroll
+                for (int c = 0; c < 3; c++) gb[c * S * S] = (1.f - fg) * G2[k][c];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        const int py = ty0 + ly0 + 4 * k;
+        BwdPix& q = P[k];
+        if (q.fi < 0) continue;
+        const float yp = pix_center(py, S);
+        const float* G = G2[k];
+        Face f = load_face_rec(frb + q.fi * FACE_REC);
+#ifndef NR_BWD_FASTDIV
+        f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
+#endif
+        bool wfast = false;
+        if (NR_ABLATE & 512) {
+            q.w[0] = f.x0, q.w[1] = f.y0, q.w[2] = f.z0;  // timing build: no weights
+        } else {
+            wfast = face_weights(xp, yp, f, q.w);
+        }
+        const float* w = q.w;
+        float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
+        if (rgb && !(NR_ABLATE & 128)) {
+            TexSample s;
+            const float* fuv = fuvb + q.fi * 8;
+            // lights: rgb = texture * cw, so the texture sees G * cw and cw sees G * texture
+            float Gt[3] = {G[0], G[1], G[2]};
+            float nrm[3], cw[3];
+            if (LIT) {
+                pixel_normal(sh, b, q.fi, w, nrm);
+                light_weights(sh, b, nrm, cw);
+#pragma unroll
+                for (int c = 0; c < 3; c++) Gt[c] = G[c] * cw[c];
+            }
+            // bilinear: images = sum_i wt_i T_i -> textures (staged below) and weights (gw)
+            float gw[4];
+            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s, Gt, gw);
+            r = s.rgb[0];
+            gg = s.rgb[1];
+            bb = s.rgb[2];
+            if (LIT) {
+                const float gcw[3] = {G[0] * r, G[1] * gg, G[2] * bb};
+                float cw2[3];
+                light_weights(sh, b, nrm, cw2, gcw, q.gn);
+                r = r * cw[0];
+                gg = gg * cw[1];
+                bb = bb * cw[2];
+            }
+            if (BG) {  // foreground: 1 * rgb + 0 * bg, as the forward computes it
+                float bgc[3];
+                background(sh, b, px, py, S, bgc);
+                r = 1.f * r + 0.f * bgc[0];
+                gg = 1.f * gg + 0.f * bgc[1];
+                bb = 1.f * bb + 0.f * bgc[2];
+            }
+            q.ay = s.y1 - s.y;
+            q.by = s.y - s.y0;
+            q.ax = s.x1 - s.x;
+            q.bx = s.x - s.x0;
+            q.grgb[0] = Gt[0];
+            q.grgb[1] = Gt[1];
+            q.grgb[2] = Gt[2];
+            if (want_tex) {
+                const bool wok = fabsf(s.lo[0]) < 1e9f && fabsf(s.lo[1]) < 1e9f;
+                const int ix0 = (int)s.x0, iy0 = (int)s.y0;
+                if (wok) {
+                    q.wx = (int)floorf(s.lo[0]);
+                    q.wy = (int)floorf(s.lo[1]);
+                }
+                const int dx = ix0 - q.wx, dy = iy0 - q.wy;
+                // corners with nonzero weight inside the window and the texture (no row wrap)
+                bool fits = wok;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float wt = ((i & 2) ? q.by : q.ay) * ((i & 1) ? q.bx : q.ax);
+                    if (wt == 0.f) continue;
+                    const int cx = dx + (i & 1), cy = dy + (i >> 1);
+                    const int gx_ = ix0 + (i & 1), gy_ = iy0 + (i >> 1);
+                    fits = fits && cx >= 0 && cx < TWIN && cy >= 0 && cy < TWIN && gx_ >= 0 && gy_ >= 0 &&
+                           gx_ < sh.tv.W && gy_ < sh.tv.H;
+                }
+                if (fits) {
+                    q.pos = dx | (dy << 8);
+                } else {
+                    // outside the face window: direct atomics (texel index as sampled)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        float* gtg = g4b + s.idx[i] * 4;
+#pragma unroll
+                        for (int ch = 0; ch < 3; ch++) {
+                            const float v = Gt[ch] * s.wt[i];
+                            if (v != 0.f && !(NR_ABLATE & 1024)) unsafeAtomicAdd(gtg + ch, v);
+                        }
+                    }
+                }
+            }
+            // texture coordinates -> z (gradient-only terms: reciprocal multiplies)
+            const float ayv = q.ay, byv = q.by, axv = q.ax, bxv = q.bx;
+            float g_x = -(gw[0] * ayv);
+            g_x = g_x + gw[1] * ayv;
+            g_x = g_x - gw[2] * byv;
+            g_x = g_x + gw[3] * byv;
+            float g_y = -(gw[0] * axv);
+            g_y = g_y - gw[1] * bxv;
+            g_y = g_y + gw[2] * axv;
+            g_y = g_y + gw[3] * bxv;
+            const float gp[2] = {g_x, g_y};
+            float gpr[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                // minimum(pc, hm) then maximum(pr, lo) backward (ties split the gradient)
+                const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
+                float gq = gp[j];
+                gq = (pc == hm) ? gq * 0.5f : (pc > hm ? 0.f : gq);
+                gq = (pr == lo) ? gq * 0.5f : (pr < lo ? 0.f : gq);
+                gpr[j] = gq;
+            }
+            const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
+            const float g_st = -g_dt * (s.dt * s.dt);
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const float rz = frcp(s.zq[j]);
+                float gzj = 0.f;
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) gzj += (-(gpr[qq] * s.dt)) * (w[j] * fuv[2 * j + qq]) * rz * rz;
+                gzj += (-g_st) * w[j] * rz * rz;
+                q.gz[j] = gzj;
+            }
+        }
+        if ((sh.draw & NR_DRAW_DEPTH) && !(NR_ABLATE & 256)) {
+            dep = depth_value(f, w, wfast);
+            // depth channel gradient reloaded (cache hit) rather than a runtime-indexed register array
+            const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
+            const float gd = upstream_one(a, gimb, py, px, S, dc);
+            const float g_s = -gd * (dep * dep);
+            const float z[3] = {f.z0, f.z1, f.z2};
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const float rz = frcp(z[j]);
+                q.gz[j] += (-g_s) * w[j] * rz * rz;
+            }
+        }
+        // channel values in merge order (rgb, sil, depth), compile-time slots as in shade_pixel
+        const bool R = rgb, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
+        I2[k][0] = R ? r : (Sl ? 1.f : dep);
+        I2[k][1] = R ? gg : dep;
+        I2[k][2] = bb;
+        I2[k][3] = Sl ? 1.f : dep;
+        I2[k][4] = dep;
+    }
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            if (c < C) {
+                s_I[c][li] = I2[k][c];
+                s_G[c][li] = G2[k][c];
+            }
+        }
+    }
+#if !NR_HALO_EARLY
+    halo_prefetch();
+#endif
+    // halo ring: image and upstream gradient only
+    int hy, hx;
+    halo_pixel(t, hy, hx);
+    const int hpy = ty0 - 1 + hy, hpx = tx0 - 1 + hx;
+    const bool h_in = t < NHALO && hpy >= 0 && hpy < S && hpx >= 0 && hpx < S;
+    if (a.halo) {
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMA halo loads have landed
+        __syncthreads();
+        if (t < NHALO) {
+            const int hl = hy * HW_ + hx;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                if (c < C) {
+                    s_I[c][hl] = h_in ? s_hI[c][t] : 0.f;
+                    s_G[c][hl] = h_in ? (a.aa ? s_hG[c][t] / 4.f : s_hG[c][t]) : 0.f;
+                }
+            }
+        }
+    } else if (t < NHALO) {
+        float hI[MAXC], hG[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
+        if (!(NR_ABLATE & 16) && h_in) {
+            const int hf = fimb[hpy * S + hpx];
+            Face ff = empty_face();
+            if (hf >= 0) ff = load_face_rec(frb + hf * FACE_REC);
+            shade_pixel(sh, b, hf, ff, hpx, hpy, S, hI);
+            upstream_grad(a, gimb, C, hpy, hpx, S, hG);
+        }
+        const int hl = hy * HW_ + hx;
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            if (c < C) {
+                s_I[c][hl] = hI[c];
+                s_G[c][hl] = hG[c];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 2. Differentiation.backward stencil -> coordinate-map gradient ------------------------
+    float gF[NPX][9];
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        const BwdPix& q = P[k];
+#pragma unroll
+        for (int j = 0; j < 9; j++) gF[k][j] = 0.f;
+        if (q.fi < 0) continue;
+        const int py = ty0 + ly0 + 4 * k;
+        const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
+        // centre values re-read from LDS (not kept in registers across the barrier)
+        float I0[MAXC], G0[MAXC], Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            const bool u = c < C;
+            I0[c] = u ? s_I[c][li] : 0.f; G0[c] = u ? s_G[c][li] : 0.f;
+            Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
+            Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
+        }
+        const float gx = (NR_ABLATE & 64) ? Im[0] : stencil(a, Im, I0, Ip, Gm, G0, Gp, px, S, C);
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            const bool u = c < C;
+            Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
+            Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
+        }
+        const float gy = (NR_ABLATE & 64) ? Ip[0] : stencil(a, Im, I0, Ip, Gm, G0, Gp, py, S, C);
+        // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            gF[k][3 * j + 0] = gx * q.w[j];
+            gF[k][3 * j + 1] = gy * q.w[j];
+            gF[k][3 * j + 2] = q.gz[j];
+        }
+    }
+    if (NR_ABLATE & 2) {
+#pragma unroll
+        for (int k = 0; k < NPX; k++)
+#pragma unroll
+            for (int j = 0; j < 9; j++) asm volatile("" ::"v"(gF[k][j]));
+        return;
+    }
+    __syncthreads();  // the staged records reuse the image / gradient LDS
+
+    // ---- 3. stage this lane's two pixel records; group the wave's records by face --------------
+    float* rec = s_raw + wid * (64 * NPX * REC);
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        float* r = rec + (k * 64 + lane) * REC;
+        reinterpret_cast<float4*>(r)[0] = make_float4(P[k].ay, P[k].by, P[k].ax, P[k].bx);
+        reinterpret_cast<float4*>(r)[1] = make_float4(__int_as_float(P[k].pos), P[k].grgb[0], P[k].grgb[1], P[k].grgb[2]);
+#pragma unroll
+        for (int j = 0; j < 9; j++) r[8 + j] = gF[k][j];
+        if (LIT) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                r[17 + j] = P[k].gn[j];
+                r[20 + j] = P[k].w[j];
+            }
+        }
+    }
+    // output lane roles: texel t = lane & 15 of the face's 4x4 window (dx = t & 3, dy = t >> 2), member
+    // chunk c = lane >> 4: lane (t, c) sums the 3 channel contributions to texel t (and, for t < 9,
+    // face-gradient float t) over the face's records whose pixel lies in row c of the wave's 16x4
+    // sub-blocks; the 4 chunks are then added across lanes.
+    const int tt = lane & 15, chunk = lane >> 4;
+    const int tdx = tt & 3, tdy = tt >> 2;
+    const int fsel = 8 + (tt < 9 ? tt : 0);
+    const int nsel_w = 20 + (tt < 9 ? tt / 3 : 0), nsel_n = 17 + (tt < 9 ? tt % 3 : 0);
+    float* __restrict__ gNb = LIT ? a.grad_normals + (long long)b * a.F * 9 : nullptr;
+    // the second pixel's state (NPX == 1: none, never active)
+    const int fi1 = NPX > 1 ? P[NPX - 1].fi : -1, wx1 = NPX > 1 ? P[NPX - 1].wx : 0, wy1 = NPX > 1 ? P[NPX - 1].wy : 0;
+    const bool act0 = P[0].fi >= 0, act1 = fi1 >= 0;
+    unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
+    // texel lanes: consecutive faces with the same texel window (e.g. every face of a flat-colour
+    // material samples one 2x2 atlas patch, load_obj.py:84-94) accumulate into `pend` and flush once
+    // per run, so such hot texels take one atomic per run instead of one per face
+    float pend = 0.f;
+    int pwx = INT_MIN, pwy = 0;
+    while (p0 | p1) {
+        // leader: lowest pending pixel; both candidates read without branches, selected on the scalar unit
+        const bool from0 = p0 != 0ull;
+        const int l0 = from0 ? __builtin_ctzll(p0) : 0, l1 = p1 ? __builtin_ctzll(p1) : 0;
+        const int k0 = __builtin_amdgcn_readlane(P[0].fi, l0), k1 = __builtin_amdgcn_readlane(fi1, l1);
+        const int x0w = __builtin_amdgcn_readlane(P[0].wx, l0), x1w = __builtin_amdgcn_readlane(wx1, l1);
+        const int y0w = __builtin_amdgcn_readlane(P[0].wy, l0), y1w = __builtin_amdgcn_readlane(wy1, l1);
+        const int key = from0 ? k0 : k1, wx = from0 ? x0w : x1w, wy = from0 ? y0w : y1w;
+        // key >= 0, so fi == key implies an active pixel
+        const unsigned long long m0 = __builtin_amdgcn_ballot_w64(P[0].fi == key) & p0;
+        const unsigned long long m1 = __builtin_amdgcn_ballot_w64(fi1 == key) & p1;
+        p0 &= ~m0;
+        p1 &= ~m1;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f, an = 0.f;
+        if (!(NR_ABLATE & 8)) {
+            // this lane's members: row `chunk` of each 16x4 sub-block (lanes 16 chunk .. 16 chunk + 15);
+            // bits 0..15 from the first pixel of each lane, 16..31 from the second
+            uint32_t mine = ((uint32_t)(m0 >> (16 * chunk)) & 0xffffu) | (((uint32_t)(m1 >> (16 * chunk)) & 0xffffu) << 16);
+            const float* rbase = rec + 16 * chunk * REC;
+            // one member's contribution: its loads issued together, accumulation predicated (no branch)
+            auto member = [&](int bit, bool on) {
+                const float* r = rbase + (((bit >> 4) * 64) + (bit & 15)) * REC;
+                const float4 ra = reinterpret_cast<const float4*>(r)[0];  // ay by ax bx
+                const float4 rb = reinterpret_cast<const float4*>(r)[1];  // pos G_r G_g G_b
+                const float rf = r[fsel];
+                float rw = 0.f, rn = 0.f;
+                if (LIT) {
+                    rw = r[nsel_w];
+                    rn = r[nsel_n];
+                }
+                const int pos = __float_as_int(rb.x);
+                const int cx = tdx - (pos & 0xff), cy = tdy - (pos >> 8);
+                const bool hit = on && pos >= 0 && cx >= 0 && cx <= 1 && cy >= 0 && cy <= 1;
+                const float wt = hit ? (cy & 1 ? ra.y : ra.x) * (cx & 1 ? ra.w : ra.z) : 0.f;
+                a0 += rb.y * wt;
+                a1 += rb.z * wt;
+                a2 += rb.w * wt;
+                af += on ? rf : 0.f;
+                if (LIT) an += on ? rw * rn : 0.f;  // corner-normal gradient tt = 3 corner + axis
+            };
+            // one loop over both pixel rows (2- and 4-member steps measured slower)
+            for (; mine; mine &= mine - 1) member(__builtin_ctz(mine), true);
+        }
+        // reduce-scatter over the 4 member chunks (lanes t, t+16, t+32, t+48) with the gfx950 lane
+        // swaps (VALU, no LDS round trip): lane (t, c) ends with the chunk total of value c
+        const float v = chunk_reduce_scatter(a0, a1, a2, af);
+        if (LIT) {  // the normal gradients: a plain sum over the 4 chunks, flushed by chunk 0
+            const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(an), __float_as_uint(an), false, false);
+            const float h = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+            const auto q2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+            const float nt = __uint_as_float(q2[0]) + __uint_as_float(q2[1]);
+            if (chunk == 0 && tt < 9 && nt != 0.f) unsafeAtomicAdd(gNb + key * 9 + tt, nt);
+        }
+        // ---- 4. flush this face: lane (t, c) writes channel c of texel t (c < 3) or face float t (c == 3)
+        if (NR_ABLATE & 4) {
+            asm volatile("" ::"v"(v));
+        } else {
+            // one atomic per lane, address selected without branches: face lanes add this face's
+            // floats; texel lanes flush the pending window when the window changes
+            const bool win = wx != INT_MIN;
+            const bool sw = win && (wx != pwx || wy != pwy);
+            const int x = pwx + tdx, y = pwy + tdy;
+            const bool tex_lane = want_tex && chunk < 3 && sw && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
+            const bool face_lane = chunk == 3 && tt < 9;
+            const float fv = face_lane ? v : pend;
+            float* dst = tex_lane ? g4b + (y * sh.tv.W + x) * 4 + chunk : gFb + key * 9 + tt;
+            if ((tex_lane || face_lane) && fv != 0.f) unsafeAtomicAdd(dst, fv);
+            if (win) {
+                pend = sw ? v : pend + v;
+                pwx = wx;
+                pwy = wy;
+            }
+        }
+    }
+    if (!(NR_ABLATE & 4)) {  // the last pending window
+        const int x = pwx + tdx, y = pwy + tdy;
+        if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
+            unsafeAtomicAdd(g4b + (y * sh.tv.W + x) * 4 + chunk, pend);
+    }
+}
+
+// pixels per lane, per launch: 2 (256 threads) when the grid fills the chip many times over; 1 (512
+// threads, 6 waves/SIMD instead of 4) for small grids, where the waves, not the per-face work, are
+// short (teapot B=4: 0.041 -> 0.035 ms; torus 1024^2 B=1: 0.059 -> 0.048 ms; on the headline and the
+// car the smaller wave regions mean more face flushes: 0.405 -> 0.417 and 0.73 -> 0.84 ms).
+// NR_BWD_NPX: 0 by grid size, 1 / 2 forced (timing builds).
+#ifndef NR_BWD_NPX
+#define NR_BWD_NPX 0
+#endif
+template <int FEAT>
+void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
+    const bool one = NR_BWD_NPX == 1 || (NR_BWD_NPX == 0 && (long long)grid.x * grid.y < 8192);
+    if (one)
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
+    else
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
+}
+
+// gathered-face gradient -> vertex gradient: gV[b, v] = sum over (f, k) with faces[f, k] = v of gF[b, f, k]
+// (the index backward of rasterize.py:232), through a CSR adjacency built once per faces tensor.
+__global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __restrict__ off,
+                              const int32_t* __restrict__ ent, float* __restrict__ gV, int F, int V, long long n,
+                              TexOut to) {
+    if (to.out) {  // this block's slice of the texture-gradient transpose
+        long long lo, hi;
+        grid_slice(to.n, lo, hi);
+        for (long long j = lo + threadIdx.x; j < hi; j += blockDim.x) tex_out_one(to, j);
+    }
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / V), v = (int)(i % V);
+    const float* base = gF + (long long)b * F * 9;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int e = off[v]; e < off[v + 1]; e++) {
+        const float* r = base + (long long)ent[e] * 3;  // entry = 3 f + k
+        s0 += r[0];
+        s1 += r[1];
+        s2 += r[2];
+    }
+    gV[i * 3 + 0] = s0;
+    gV[i * 3 + 1] = s1;
+    gV[i * 3 + 2] = s2;
+}
+
+// vertex-normal backward (lights): gU[b, v] = d/du of F.normalize (rasterize.py:182) applied to the
+// gradient of n[b, v], gathered over the vertex's face corners (the gather at rasterize.py:183)
+__global__ void k_vnormal_bwd(const float* __restrict__ gN, const int32_t* __restrict__ off,
+                              const int32_t* __restrict__ ent, const float* __restrict__ vnorm,
+                              float* __restrict__ gU, int F, int V, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / V), v = (int)(i % V);
+    const float* base = gN + (long long)b * F * 9;
+    float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+    for (int e = off[v]; e < off[v + 1]; e++) {
+        const float* r = base + ent[e] * 3;  // entry = 3 f + k
+        g0 += r[0];
+        g1 += r[1];
+        g2 += r[2];
+    }
+    const float4 nv = reinterpret_cast<const float4*>(vnorm)[i];  // n = u / max(|u|, eps), |u|
+    float* o = gU + i * 3;
+    if (nv.w > 1e-12f) {
+        // d(u / |u|)/du^T g = (g - n (n . g)) / |u|
+        const float nd = (nv.x * g0 + nv.y * g1) + nv.z * g2;
+        o[0] = (g0 - nv.x * nd) / nv.w;
+        o[1] = (g1 - nv.y * nd) / nv.w;
+        o[2] = (g2 - nv.z * nd) / nv.w;
+    } else {
+        o[0] = g0 / 1e-12f;
+        o[1] = g1 / 1e-12f;
+        o[2] = g2 / 1e-12f;
+    }
+}
+
+// face-normal backward (lights): the face normal gets the gradients of its distinct vertices' sums
+// (the one-hot matmul, rasterize.py:173-179), then n = a x b with a = v1 - v0, b = v2 - v1 gives
+// dL/da = b x g, dL/db = g x a, added to the face's corner gradients gF (rasterize.py:166-170)
+__global__ void k_fnormal_bwd(const float* __restrict__ face_records, const int32_t* __restrict__ fidx,
+                              const float* __restrict__ gU, float* __restrict__ gF, int F, int V, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / F), f = (int)(i % F);
+    const int v0 = fidx[f * 3], v1 = fidx[f * 3 + 1], v2 = fidx[f * 3 + 2];
+    const float* ub = gU + (long long)b * V * 3;
+    float g[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        g[j] = ub[v0 * 3 + j];
+        if (v1 != v0) g[j] += ub[v1 * 3 + j];
+        if (v2 != v0 && v2 != v1) g[j] += ub[v2 * 3 + j];
+    }
+    const float* c = face_records + i * FACE_REC;
+    const float a0 = c[3] - c[0], a1 = c[4] - c[1], a2 = c[5] - c[2];
+    const float b0 = c[6] - c[3], b1 = c[7] - c[4], b2 = c[8] - c[5];
+    const float da0 = b1 * g[2] - b2 * g[1], da1 = b2 * g[0] - b0 * g[2], da2 = b0 * g[1] - b1 * g[0];
+    const float db0 = g[1] * a2 - g[2] * a1, db1 = g[2] * a0 - g[0] * a2, db2 = g[0] * a1 - g[1] * a0;
+    float* o = gF + i * 9;
+    o[0] -= da0;
+    o[1] -= da1;
+    o[2] -= da2;
+    o[3] += da0 - db0;
+    o[4] += da1 - db1;
+    o[5] += da2 - db2;
+    o[6] += db0;
+    o[7] += db1;
+    o[8] += db2;
+}
+
+// [Bt, HWp, 4] accumulation layout -> [Bt, 3, H, W]
+__global__ void k_tex_out(TexOut to) {  // standalone form (no vertex gradient to carry it)
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < to.n) tex_out_one(to, i);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_param_bwd: the gradients of the inputs that only the rgb channels see and that the main backward
+// does not produce -- vertices_textures (UV) and the light parameters (LGT).  One thread per internal
+// pixel (a wave = 64 pixels of one row); runs only when one of them is requested.
+//   UV:  sample_textures (rasterize.py:111-121): x = min(max(pr, lo), hm) with pr = num * dt,
+//        num = sum_k (w_k uv_k) / zq_k, lo = min_k uv_k, hm = max_k uv_k - eps.  The bilinear weight
+//        gradient (as in k_raster_bwd) goes back through the two clamps (ties split in half, as
+//        torch.maximum / torch.minimum do), to pr -> uv_k through (w_k / zq_k) dt, and to the
+//        first-occurring arg-min / arg-max corner (torch's min(-2) / max(-2) backward).  Lanes of
+//        one face are summed across the wave and the leader adds the 6 corner values to
+//        grad_vt[faces_textures[f, k]] (the gather backward of rasterize.py:246).
+//   LGT: the light loop (rasterize.py:252-283) with rgb = T cw, dL/dcw = G T: per light, the colour
+//        gets s dL/dcw, a directional light's direction gets -n s'(raw) sum_c(dL/dcw_c col_c), a
+//        specular exponent gets sum_c(dL/dcw_c col_c) s^alpha log(s) (0 where s == 0, alpha >= 0, as
+//        torch's pow backward).  Wave sums, one atomic per wave and value into grad_lights, laid
+//        out like the light records [L][B][NR_LIGHT_FLOATS] (colour 2..4, direction 5..7, alpha 5).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <bool UV, bool LGT>
+__global__ __launch_bounds__(256) void k_param_bwd(BwdArgs a, Shade sh, int S, const int32_t* __restrict__ ftex,
+                                                   float* __restrict__ grad_vt, long long gvt_bstride,
+                                                   float* __restrict__ grad_lights) {
+    const int b = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool inside = p < S * S;
+    const int y = inside ? p / S : 0, x = inside ? p - y * S : 0;
+    const int fi = inside ? a.fim[(long long)b * S * S + p] : -1;
+    const int bt = sh.tv.sb ? b : 0;
+    float guv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float T[3] = {0.f, 0.f, 0.f}, G[MAXC], nrm[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < MAXC; c++) G[c] = 0.f;
+    if (fi >= 0) {
+        const float* gimb = a.grad_images + (long long)b * sh.C * (a.aa ? a.s * a.s : S * S);
+        upstream_grad(a, gimb, sh.C, y, x, S, G);
+        Face f = load_face_rec(a.face_records + ((long long)b * a.F + fi) * FACE_REC);
+        f.flags = 0;
+        float w[3];
+        face_weights(pix_center(x, S), pix_center(y, S), f, w);
+        float Gt[3] = {G[0], G[1], G[2]};
+        float cw[3];
+        if (sh.nl) {
+            pixel_normal(sh, b, fi, w, nrm);
+            light_weights(sh, b, nrm, cw);
+#pragma unroll
+            for (int c = 0; c < 3; c++) Gt[c] = G[c] * cw[c];
+        }
+        const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + fi * 8;
+        TexSample s;
+        float gw[4];
+        sample_texture(f, w, false, fuv, sh.tv, bt, sh.eps, s, Gt, gw);
+        T[0] = s.rgb[0];
+        T[1] = s.rgb[1];
+        T[2] = s.rgb[2];
+        if (UV) {
+            const float ay = s.y1 - s.y, by = s.y - s.y0, ax = s.x1 - s.x, bx = s.x - s.x0;
+            const float gp[2] = {((-(gw[0] * ay) + gw[1] * ay) - gw[2] * by) + gw[3] * by,
+                                 ((-(gw[0] * ax) - gw[1] * bx) + gw[2] * ax) + gw[3] * bx};
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const float pc = s.pc[j], hm = s.hm[j], pr = s.pr[j], lo = s.lo[j];
+                const float g = gp[j];
+                const float to_pc = pc == hm ? g * 0.5f : (pc < hm ? g : 0.f);
+                const float to_hm = pc == hm ? g * 0.5f : (pc > hm ? g : 0.f);
+                const float to_pr = pr == lo ? to_pc * 0.5f : (pr > lo ? to_pc : 0.f);
+                const float to_lo = pr == lo ? to_pc * 0.5f : (pr < lo ? to_pc : 0.f);
+                const float gnum = to_pr * s.dt;
+                const float u[3] = {fuv[j], fuv[2 + j], fuv[4 + j]};
+                const int kmin = (u[1] < u[0] && !(u[2] < u[1])) ? 1 : ((u[2] < u[0] && u[2] < u[1]) ? 2 : 0);
+                const int kmax = (u[1] > u[0] && !(u[2] > u[1])) ? 1 : ((u[2] > u[0] && u[2] > u[1]) ? 2 : 0);
+#pragma unroll
+                for (int k = 0; k < 3; k++)
+                    guv[2 * k + j] = (gnum / s.zq[k]) * w[k] + (k == kmin ? to_lo : 0.f) + (k == kmax ? to_hm : 0.f);
+            }
+        }
+    }
+    if (UV) {
+        // group the wave's lanes by face; the leader adds the face's 6 sums to its uv vertices
+        const bool act = fi >= 0;
+        unsigned long long pend = __ballot(act);
+        float* gvb = grad_vt + (sh.uv_bstride ? (long long)b * gvt_bstride : 0);
+        while (pend) {
+            const int leader = __builtin_ctzll(pend);
+            const int key = __builtin_amdgcn_readlane(fi, leader);
+            const bool mem = act && fi == key;
+            pend &= ~__ballot(mem);
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                const float v = wave_sum(mem ? guv[q] : 0.f);
+                if (lane == leader && v != 0.f) unsafeAtomicAdd(gvb + ftex[key * 3 + q / 2] * 2 + (q & 1), v);
+            }
+        }
+    }
+    if (LGT) {
+        const bool act = fi >= 0;
+        const float gcw[3] = {G[0] * T[0], G[1] * T[1], G[2] * T[2]};
+        for (int l = 0; l < sh.nl; l++) {
+            const float* L = sh.lights + ((long long)l * sh.B + b) * NR_LIGHT_FLOATS;
+            float* gl = grad_lights + ((long long)l * sh.B + b) * NR_LIGHT_FLOATS;
+            const int kind = (int)L[0];
+            const bool back = L[1] != 0.f;
+            const float col[3] = {L[2], L[3], L[4]};
+            float gc[3], gd[3] = {0.f, 0.f, 0.f}, ga = 0.f;
+            if (kind == NR_LIGHT_AMBIENT) {
+                gc[0] = gcw[0], gc[1] = gcw[1], gc[2] = gcw[2];
+            } else {
+                const bool dirl = kind == NR_LIGHT_DIRECTIONAL;
+                const float d0 = dirl ? L[5] : 0.f, d1 = dirl ? L[6] : 0.f, d2 = dirl ? L[7] : 1.f;
+                const float raw = ((-d0) * nrm[0] + (-d1) * nrm[1]) + (-d2) * nrm[2];
+                const float sv = back ? fabsf(raw) : t_relu(raw);
+                const float ds = back ? (raw > 0.f ? 1.f : (raw < 0.f ? -1.f : 0.f)) : (raw > 0.f ? 1.f : 0.f);
+                const float gs = (gcw[0] * col[0] + gcw[1] * col[1]) + gcw[2] * col[2];
+                if (dirl) {
+#pragma unroll
+                    for (int c = 0; c < 3; c++) gc[c] = sv * gcw[c];
+                    gd[0] = gs * ds * (-nrm[0]);
+                    gd[1] = gs * ds * (-nrm[1]);
+                    gd[2] = gs * ds * (-nrm[2]);
+                } else {
+                    const float alpha = L[5];
+                    const float pw = powf(sv, alpha);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) gc[c] = pw * gcw[c];
+                    ga = (sv == 0.f && alpha >= 0.f) ? 0.f : gs * (pw * logf(sv));
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float v = wave_sum(act ? gc[c] : 0.f);
+                if (lane == 0 && v != 0.f) unsafeAtomicAdd(gl + 2 + c, v);
+            }
+            if (kind == NR_LIGHT_DIRECTIONAL) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float v = wave_sum(act ? gd[c] : 0.f);
+                    if (lane == 0 && v != 0.f) unsafeAtomicAdd(gl + 5 + c, v);
+                }
+            } else if (kind == NR_LIGHT_SPECULAR) {
+                const float v = wave_sum(act ? ga : 0.f);
+                if (lane == 0 && v != 0.f) unsafeAtomicAdd(gl + 5, v);
+            }
+        }
+    }
+}
+
+}  // namespace

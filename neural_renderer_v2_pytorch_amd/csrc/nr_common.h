@@ -1,0 +1,598 @@
+// nr_common.h -- errors, profiling hook, geometry, the exact-division helpers, per-pixel shading (weights, texture sample, depth, lights, backgrounds), XCD tile map, block scan, texture repack helpers
+// Part of nr_raster.hip (one translation unit); see that file and DESIGN.md.
+#pragma once
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int TW = 32;             // tile width  (internal pixels)
+constexpr int TH = 8;              // tile height
+constexpr int NT = TW * TH;        // threads per raster block, one pixel each
+constexpr int COARSE = 32;         // coarse bin edge (pixels) = forward block region; = TW, multiple of TH
+constexpr int SETUP_FACES = 128;   // faces per setup block (4 bitmask words)
+constexpr int SETUP_LDS_WORDS = 4096;  // bin-mask words built in LDS (up to 1024 bins, S <= 1024)
+constexpr int MAXC = 5;            // max output channels
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipPeekAtLastError();
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(NR_ERR_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+    }
+    return NR_OK;
+}
+
+// ---- measurement hook (nr_profile_enable / nr_profile_read) ----
+enum { P_SETUP, P_RASTER, P_SHADE, P_BWD, P_VGRAD, P_TEXOUT, P_TEXPACK, P_N };
+const char* const kProfNames[P_N] = {"k_face_setup", "k_raster_fwd", "k_shade",
+                                     "k_raster_bwd", "k_vertex_grad", "k_tex_out", "k_tex_pack"};
+bool g_prof = false;
+hipEvent_t g_prof_ev[P_N][2];
+bool g_prof_rec[P_N];
+
+struct ProfScope {  // records the start/end events of one launch when profiling is on
+    int k;
+    hipStream_t st;
+    ProfScope(int k_, hipStream_t s) : k(k_), st(s) {
+        if (g_prof) (void)hipEventRecord(g_prof_ev[k][0], st);
+    }
+    ~ProfScope() {
+        if (g_prof) {
+            (void)hipEventRecord(g_prof_ev[k][1], st);
+            g_prof_rec[k] = true;
+        }
+    }
+};
+
+struct Geom {
+    int S, nbx, nby, nbins, nwords, tiles_x, tiles_y;
+};
+
+Geom make_geom(int F, int S) {
+    Geom g;
+    g.S = S;
+    g.nbx = (S + COARSE - 1) / COARSE;
+    g.nby = g.nbx;
+    g.nbins = g.nbx * g.nby;
+    g.nwords = (F + 31) / 32;
+    g.tiles_x = (S + TW - 1) / TW;
+    g.tiles_y = (S + TH - 1) / TH;
+    return g;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// workspace layout: [bbox int2 B*F][mask u32 B*nbins*nwords]
+size_t ws_bbox_bytes(int B, int F) { return align_up((size_t)B * F * sizeof(int2)); }
+size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins * g.nwords * 4); }
+
+// ------------------------------------------------------------------------------------------------
+// device helpers
+
+// rasterize_cuda_kernel.cu:76-77: pixel centre, computed in double, rounded to float
+__device__ __forceinline__ float pix_center(int i, int S) { return (float)((2. * i + 1 - S) / S); }
+
+// conservative range of pixel indices whose centre may lie in [lo, hi] (float compare).  Empty
+// when lo > hi.  One pixel of margin on each side absorbs the float rounding of the centres.
+__device__ __forceinline__ void pix_range(float lo, float hi, int S, int& i0, int& i1) {
+    double a = ((double)lo * S + S - 1) * 0.5;
+    double b = ((double)hi * S + S - 1) * 0.5;
+    a = fmin(fmax(a, -2.0), (double)S + 2.0);
+    b = fmin(fmax(b, -2.0), (double)S + 2.0);
+    i0 = max((int)ceil(a) - 1, 0);
+    i1 = min((int)floor(b) + 1, S - 1);
+}
+
+__device__ __forceinline__ int pack_range(int lo, int hi) { return (lo & 0xffff) | (hi << 16); }
+// an empty range never overlaps anything: lo = 32767 > any pixel index, hi = -1
+#define NR_EMPTY_RANGE ((int)0xffff7fff)
+__device__ __forceinline__ int range_lo(int p) { return p & 0xffff; }
+__device__ __forceinline__ int range_hi(int p) { return p >> 16; }
+
+// A gathered face.  The fused path keeps 16-float face records (FACE_REC floats, 64 B, one aligned
+// load of 4 x float4): the 9 corner coordinates, then per-face reciprocals for the exact division
+// shortcut (rcp_nr(z_k), rcp_nr(z_k + 1e-10)) and the operand-range flags that allow it.  Faces
+// handed over by the caller (face_index_map_forward_safe, compute_weight_map) are 9 floats and
+// always take the plain IEEE divisions (flags = 0).
+constexpr int FACE_REC = 16;
+constexpr int FACE_FAST_XYZ = 1;  // x, y in {0} u [2^-20, 2^20], |z| in [2^-20, 2^20]
+constexpr int FACE_FAST_ZQ = 2;   // |z + 1e-10| in [2^-20, 2^20]
+struct Face {
+    float x0, y0, z0, x1, y1, z1, x2, y2, z2;
+    float rz0, rz1, rz2, rq0, rq1, rq2;
+    int flags;
+};
+
+__device__ __forceinline__ Face load_face(const float* __restrict__ fr) {
+    Face f;
+    f.x0 = fr[0]; f.y0 = fr[1]; f.z0 = fr[2];
+    f.x1 = fr[3]; f.y1 = fr[4]; f.z1 = fr[5];
+    f.x2 = fr[6]; f.y2 = fr[7]; f.z2 = fr[8];
+    f.rz0 = f.rz1 = f.rz2 = f.rq0 = f.rq1 = f.rq2 = 0.f;
+    f.flags = 0;
+    return f;
+}
+
+__device__ __forceinline__ Face load_face_rec(const float* __restrict__ fr) {
+    const float4* p = reinterpret_cast<const float4*>(fr);
+    const float4 a = p[0], b = p[1], c = p[2], d = p[3];
+    Face f;
+    f.x0 = a.x; f.y0 = a.y; f.z0 = a.z;
+    f.x1 = a.w; f.y1 = b.x; f.z1 = b.y;
+    f.x2 = b.z; f.y2 = b.w; f.z2 = c.x;
+    f.rz0 = c.y; f.rz1 = c.z; f.rz2 = c.w;
+    f.rq0 = d.x; f.rq1 = d.y; f.rq2 = d.z;
+    f.flags = __float_as_int(d.w);
+    return f;
+}
+
+__device__ __forceinline__ Face empty_face() {
+    Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    return f;
+}
+
+// torch.maximum / torch.minimum / min(-2) / max(-2) semantics: NaN propagates
+__device__ __forceinline__ float t_max(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a > b ? a : b); }
+__device__ __forceinline__ float t_min(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a < b ? a : b); }
+
+// ---- exact division without the scaling / fix-up steps --------------------------------------
+// gfx950 lowers an IEEE binary32 a / b to
+//   v_div_scale(b), v_rcp, v_div_scale(a), r = fma(fma(-b, rcp, 1), rcp, rcp), q = a * r,
+//   q = fma(fma(-b, q, a), r, q), v_div_fmas(fma(-b, q, a), r, q), v_div_fixup.
+// v_div_scale leaves its operand unchanged and clears VCC, and v_div_fixup returns its input, unless
+// an operand is zero / inf / NaN / denormal, the quotient or 1/b is denormal, the numerator is below
+// 2^-103, or the exponents differ by 96 or more.  Outside those cases the sequence is exactly
+// rcp_nr + div_nr below, so div_nr is bit-identical to a / b there, and a reciprocal shared by
+// several divisions by the same b is computed once.  Callers guard the operand ranges (DESIGN.md
+// "Numerics"); a zero numerator may come out as +0 where a / b gives -0, which no caller observes.
+__device__ __forceinline__ float rcp_nr(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, r, 1.f), r, r);
+}
+__device__ __forceinline__ float div_nr(float a, float b, float r) {
+    float q = a * r;
+    q = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+// |x| in [2^-e, 2^e]
+__device__ __forceinline__ bool in_range(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }
+// coordinate / depth magnitudes for which the face-level guard below holds: 0 or [2^-20, 2^20]
+__device__ __forceinline__ bool coord_ok(float x) { return x == 0.f || in_range(x, 0x1p-20f, 0x1p20f); }
+
+// compute_weight_map_cuda_kernel (.cu:286-306).  Returns true when the weights are known to lie in
+// {0} u [2^-84, 1] (the exact-division path was taken), which the texture and depth stages below
+// need for their own shortcut.
+__device__ __forceinline__ bool face_weights(float xp, float yp, const Face& f, float w[3]) {
+    w[0] = yp * (f.x2 - f.x1) + xp * (f.y1 - f.y2) + (f.x1 * f.y2 - f.x2 * f.y1);
+    w[1] = yp * (f.x0 - f.x2) + xp * (f.y2 - f.y0) + (f.x2 * f.y0 - f.x0 * f.y2);
+    w[2] = yp * (f.x1 - f.x0) + xp * (f.y0 - f.y1) + (f.x0 * f.y1 - f.x1 * f.y0);
+    float s = w[0] + w[1] + w[2];
+    if (s < 0) {
+        w[0] = -w[0];
+        w[1] = -w[1];
+        w[2] = -w[2];
+    }
+    w[0] = fmaxf(w[0], 0.f);
+    w[1] = fmaxf(w[1], 0.f);
+    w[2] = fmaxf(w[2], 0.f);
+    s = w[0] + w[1] + w[2];
+    // with FACE_FAST_XYZ every w is 0 or in [2^-80, 2^42] (DESIGN.md "Numerics")
+    if ((f.flags & FACE_FAST_XYZ) && in_range(s, 0x1p-20f, 0x1p4f)) {
+        const float r = rcp_nr(s);
+#pragma unroll
+        for (int j = 0; j < 3; j++) w[j] = fmaxf(fminf(div_nr(w[j], s, r), 1.f), 0.f);
+        return true;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) w[j] = fmaxf(fminf(w[j] / s, 1.f), 0.f);
+    return false;
+}
+
+// 1 / x through div_nr's range (|x| in [2^-90, 2^90]), else IEEE
+__device__ __forceinline__ float recip_exact(float x) {
+    if (in_range(x, 0x1p-90f, 0x1p90f)) {
+        const float r = rcp_nr(x);
+        const float q = __builtin_fmaf(__builtin_fmaf(-x, r, 1.f), r, r);  // div_nr(1, x, r): 1 * r == r
+        return __builtin_fmaf(__builtin_fmaf(-x, q, 1.f), r, q);
+    }
+    return 1.f / x;
+}
+
+struct TexView {
+    const float* __restrict__ tex;
+    long long sb;   // item stride (uniform 64-bit part)
+    int sc, sp;     // channel / texel strides: one item's view spans < 2^31 elements (validate_raster)
+    int H, W;
+    // the same texels packed as RGBA rows [Bt][HWp] (NrRasterArgs.textures_packed), or null: one 16-B
+    // load per bilinear corner, and 2 cache lines per pixel instead of 6 (3 channel planes x 2 rows)
+    const float4* __restrict__ t4;
+    int HWp;
+};
+
+__device__ __forceinline__ float texel(const TexView& t, int b, int c, int p) {
+    return t.tex[(long long)b * t.sb + (c * t.sc + p * t.sp)];
+}
+
+// sample_textures (rasterize.py:100-153) for one foreground pixel, with the intermediates the
+// backward needs.
+struct TexSample {
+    float zq[3];        // z_k + 1e-10
+    float dt;           // 1 / sum(w/(z+1e-10) + 1e-10)
+    float num[2];       // sum_k (w_k uv_k)/(z_k + 1e-10)
+    float pr[2];        // num * dt (pre-clamp)
+    float pc[2];        // after the lower clamp
+    float hm[2];        // upper bound (max uv - eps)
+    float lo[2];
+    float x, y, x0, y0, x1, y1;
+    int idx[4];
+    float wt[4];
+    float rgb[3];
+};
+
+// uv: the face's 8-float texture record (u0 v0 u1 v1 u2 v2, flag, -); flag 1 = every u, v in
+// {0} u [2^-16, 2^20].  wfast: face_weights took its exact-division path.
+// G (optional, backward): upstream gradient of the rgb channels; then gw[i] = sum_c G[c] T_i[c] for
+// the 4 bilinear texels, from the texel values loaded here (no second load)
+__device__ __forceinline__ void sample_texture(const Face& f, const float w[3], bool wfast, const float* __restrict__ uv,
+                                               const TexView& tv, int bt, float eps, TexSample& s,
+                                               const float* G = nullptr, float* gw = nullptr) {
+    const float4 uva = reinterpret_cast<const float4*>(uv)[0], uvb = reinterpret_cast<const float4*>(uv)[1];
+    const float uvs[6] = {uva.x, uva.y, uva.z, uva.w, uvb.x, uvb.y};
+    const bool fast = wfast && (f.flags & FACE_FAST_ZQ) && __float_as_int(uvb.z) != 0;
+    const float z[3] = {f.z0, f.z1, f.z2};
+    const float rq[3] = {f.rq0, f.rq1, f.rq2};
+    float st = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        s.zq[k] = z[k] + 1e-10f;
+        const float t = (fast ? div_nr(w[k], s.zq[k], rq[k]) : w[k] / s.zq[k]) + 1e-10f;
+        st = (k == 0) ? t : st + t;
+    }
+    s.dt = fast ? recip_exact(st) : 1.f / st;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const float u0 = uvs[j], u1 = uvs[2 + j], u2 = uvs[4 + j];
+        if (fast)
+            s.num[j] = (div_nr(w[0] * u0, s.zq[0], rq[0]) + div_nr(w[1] * u1, s.zq[1], rq[1])) +
+                       div_nr(w[2] * u2, s.zq[2], rq[2]);
+        else
+            s.num[j] = ((w[0] * u0) / s.zq[0] + (w[1] * u1) / s.zq[1]) + (w[2] * u2) / s.zq[2];
+        s.pr[j] = s.num[j] * s.dt;
+        s.lo[j] = t_min(t_min(u0, u1), u2);
+        s.hm[j] = t_max(t_max(u0, u1), u2) - eps;
+        s.pc[j] = t_max(s.pr[j], s.lo[j]);
+    }
+    s.x = t_min(s.pc[0], s.hm[0]);
+    s.y = t_min(s.pc[1], s.hm[1]);
+    s.x0 = floorf(s.x);
+    s.y0 = floorf(s.y);
+    s.x1 = s.x0 + 1;
+    s.y1 = s.y0 + 1;
+    const int xi0 = (int)s.x0, yi0 = (int)s.y0, xi1 = (int)s.x1, yi1 = (int)s.y1;
+    const int W = tv.W, HW = tv.H * tv.W;
+    s.idx[0] = yi0 * W + xi0;
+    s.idx[1] = yi0 * W + xi1;
+    s.idx[2] = yi1 * W + xi0;
+    s.idx[3] = yi1 * W + xi1;
+#pragma unroll
+    for (int i = 0; i < 4; i++) s.idx[i] = min(max(s.idx[i], 0), HW - 1);  // weight-0 overhang, SURVEY A9
+    s.wt[0] = (s.y1 - s.y) * (s.x1 - s.x);
+    s.wt[1] = (s.y1 - s.y) * (s.x - s.x0);
+    s.wt[2] = (s.y - s.y0) * (s.x1 - s.x);
+    s.wt[3] = (s.y - s.y0) * (s.x - s.x0);
+    const float* tb = tv.tex + (long long)bt * tv.sb;
+    int off[4];
+    float4 q4[4];
+    if (tv.t4) {
+        const float4* t4b = tv.t4 + (long long)bt * tv.HWp;
+#pragma unroll
+        for (int i = 0; i < 4; i++) q4[i] = t4b[s.idx[i]];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) off[i] = s.idx[i] * tv.sp;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const float* tc = tb + c * tv.sc;
+        float t0, t1, t2, t3;
+        if (tv.t4) {
+            t0 = c == 0 ? q4[0].x : (c == 1 ? q4[0].y : q4[0].z);
+            t1 = c == 0 ? q4[1].x : (c == 1 ? q4[1].y : q4[1].z);
+            t2 = c == 0 ? q4[2].x : (c == 1 ? q4[2].y : q4[2].z);
+            t3 = c == 0 ? q4[3].x : (c == 1 ? q4[3].y : q4[3].z);
+        } else {
+            t0 = tc[off[0]], t1 = tc[off[1]], t2 = tc[off[2]], t3 = tc[off[3]];
+        }
+        s.rgb[c] = ((s.wt[0] * t0 + s.wt[1] * t1) + s.wt[2] * t2) + s.wt[3] * t3;
+        if (G) {
+            if (c == 0) {
+                gw[0] = G[0] * t0;
+                gw[1] = G[0] * t1;
+                gw[2] = G[0] * t2;
+                gw[3] = G[0] * t3;
+            } else {
+                gw[0] = gw[0] + G[c] * t0;
+                gw[1] = gw[1] + G[c] * t1;
+                gw[2] = gw[2] + G[c] * t2;
+                gw[3] = gw[3] + G[c] * t3;
+            }
+        }
+    }
+}
+
+// compute_depth_map (rasterize.py:80-88) for a foreground pixel
+__device__ __forceinline__ float depth_value(const Face& f, const float w[3], bool wfast) {
+    if (wfast) {  // weights in {0} u [2^-84, 1], |z| in [2^-20, 2^20]
+        return recip_exact((div_nr(w[0], f.z0, f.rz0) + div_nr(w[1], f.z1, f.rz1)) + div_nr(w[2], f.z2, f.rz2));
+    }
+    return 1.f / ((w[0] / f.z0 + w[1] / f.z1) + w[2] / f.z2);
+}
+
+struct Shade {
+    int draw;       // NR_DRAW_* flags
+    int C;          // channels
+    float eps;
+    TexView tv;
+    const float* __restrict__ face_uv;
+    long long uv_bstride;  // F*8 or 0
+    // lights (rgb only): records [nl][B][NR_LIGHT_FLOATS], vertex normals [B, V, 4], face corners
+    int nl, B, V;
+    const float* __restrict__ lights;
+    const float* __restrict__ vnorm;
+    const int32_t* __restrict__ fidx;
+    // backgrounds (rgb only): [B, 3, S, S], x stride 1
+    const float* __restrict__ bg;
+    long long bg_sb;
+    int bg_sc, bg_sy;
+};
+
+// torch.relu (NaN stays NaN)
+__device__ __forceinline__ float t_relu(float x) { return x > 0.f ? x : (x != x ? x : 0.f); }
+
+// smooth normal map at a pixel of face fi (rasterize.py:185-187): sum_k w_k n_k over the face's
+// corner vertex normals, per component ((w0 n0 + w1 n1) + w2 n2)
+__device__ __forceinline__ void pixel_normal(const Shade& sh, int b, int fi, const float w[3], float n[3]) {
+    const float* vb = sh.vnorm + (long long)b * sh.V * 4;
+    float c[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float4 v = *reinterpret_cast<const float4*>(vb + sh.fidx[fi * 3 + k] * 4);
+        c[k][0] = v.x;
+        c[k][1] = v.y;
+        c[k][2] = v.z;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) n[j] = (w[0] * c[0][j] + w[1] * c[1][j]) + w[2] * c[2][j];
+}
+
+// the light loop of rasterize.py:252-281 for one pixel: colour weights cw (starting from 0, lights
+// added in list order); with gcw != nullptr, instead accumulate dL/dn into gn given dL/dcw = gcw
+__device__ __forceinline__ void light_weights(const Shade& sh, int b, const float n[3], float cw[3],
+                                              const float* gcw = nullptr, float* gn = nullptr) {
+    cw[0] = cw[1] = cw[2] = 0.f;
+    for (int l = 0; l < sh.nl; l++) {
+        const float* L = sh.lights + ((long long)l * sh.B + b) * NR_LIGHT_FLOATS;
+        const int kind = (int)L[0];
+        const bool back = L[1] != 0.f;
+        const float col[3] = {L[2], L[3], L[4]};
+        if (kind == NR_LIGHT_AMBIENT) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) cw[c] = cw[c] + col[c];
+            continue;
+        }
+        // intensity = sum(-d * n) with d the light direction, or (0, 0, 1) for specular
+        const float d0 = kind == NR_LIGHT_DIRECTIONAL ? L[5] : 0.f;
+        const float d1 = kind == NR_LIGHT_DIRECTIONAL ? L[6] : 0.f;
+        const float d2 = kind == NR_LIGHT_DIRECTIONAL ? L[7] : 1.f;
+        const float raw = ((-d0) * n[0] + (-d1) * n[1]) + (-d2) * n[2];
+        float s = back ? fabsf(raw) : t_relu(raw);
+        const float alpha = L[5];
+        float ds = back ? (raw > 0.f ? 1.f : (raw < 0.f ? -1.f : 0.f)) : (raw > 0.f ? 1.f : 0.f);  // d s / d raw
+        if (kind == NR_LIGHT_SPECULAR) {
+            const float p = powf(s, alpha);
+            ds = ds * (alpha * powf(s, alpha - 1.f));  // torch pow backward: exponent * base^(exponent - 1)
+            s = p;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) cw[c] = cw[c] + s * col[c];
+        if (gn) {
+            const float gs = ((gcw[0] * col[0] + gcw[1] * col[1]) + gcw[2] * col[2]) * ds;
+            gn[0] += gs * (-d0);
+            gn[1] += gs * (-d1);
+            gn[2] += gs * (-d2);
+        }
+    }
+}
+
+// background colour of internal pixel (x, y): backgrounds[b, c, S-1-y, S-1-x]
+__device__ __forceinline__ void background(const Shade& sh, int b, int x, int y, int S, float bgc[3]) {
+    const float* p = sh.bg + (long long)b * sh.bg_sb + (S - 1 - y) * sh.bg_sy + (S - 1 - x);
+#pragma unroll
+    for (int c = 0; c < 3; c++) bgc[c] = p[c * sh.bg_sc];
+}
+
+// All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth), written
+// to compile-time slots of out[MAXC] (runtime-indexed register arrays would spill to scratch).
+__device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, int x, int y, int S,
+                                            float* out) {
+    const bool R = (sh.draw & NR_DRAW_RGB) != 0, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
+    const float xp = pix_center(x, S), yp = pix_center(y, S);
+    float r = 0.f, gg = 0.f, bb = 0.f, sil = 0.f, dep = 0.f;
+    if (fi >= 0) {
+        float w[3];
+        const bool wfast = face_weights(xp, yp, f, w);
+        if (R) {
+            TexSample s;
+            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + fi * 8;
+            sample_texture(f, w, wfast, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s);
+            r = s.rgb[0];
+            gg = s.rgb[1];
+            bb = s.rgb[2];
+            if (sh.nl) {  // rgb_map *= color_weight_map (rasterize.py:283)
+                float n[3], cw[3];
+                pixel_normal(sh, b, fi, w, n);
+                light_weights(sh, b, n, cw);
+                r = r * cw[0];
+                gg = gg * cw[1];
+                bb = bb * cw[2];
+            }
+        }
+        sil = 1.f;
+        if (sh.draw & NR_DRAW_DEPTH) dep = depth_value(f, w, wfast);
+    }
+    if (R && sh.bg) {  // fg * rgb + (1 - fg) * bg (chainer rasterize.py:576)
+        float bgc[3];
+        background(sh, b, x, y, S, bgc);
+        const float fg = fi >= 0 ? 1.f : 0.f;
+        r = fg * r + (1.f - fg) * bgc[0];
+        gg = fg * gg + (1.f - fg) * bgc[1];
+        bb = fg * bb + (1.f - fg) * bgc[2];
+    }
+    out[0] = R ? r : (Sl ? sil : dep);
+    out[1] = R ? gg : dep;
+    out[2] = bb;
+    out[3] = Sl ? sil : dep;
+    out[4] = dep;
+}
+
+// ------------------------------------------------------------------------------------------------
+// XCD-aware block -> tile map.  Workgroups go round-robin to the 8 XCDs (linear id % 8) and each XCD
+// has its own L2, so with the identity map horizontally adjacent tiles never share a cache, and the
+// halo columns, upstream-gradient lines and face records they have in common are fetched once per
+// XCD.  Two remaps (measured on the headline workload):
+//   mode 1 (groups): runs of SW x SH neighbouring tiles go to one XCD back to back; groups
+//          interleave over the XCDs.  Full tile rows (SW = nx, SH = 1) are the balanced case.
+//   mode 2 (bands):  XCD x takes a band of ny / 8 whole tile rows of each item, the band rotating
+//          with the item so every XCD sees every band over 8 items (balanced over the batch).
+// Both fall back to the identity when the grid does not divide evenly (the linear id of item b
+// starts at b * nx * ny, a multiple of 8 whenever the remap applies).
+#ifndef NR_SWZ_MODE
+#define NR_SWZ_MODE 2
+#endif
+#ifndef NR_SWZ_W
+#define NR_SWZ_W 0  // 0: the full tile row
+#endif
+#ifndef NR_SWZ_H
+#define NR_SWZ_H 1
+#endif
+#ifndef NR_FSWZ_MODE
+#define NR_FSWZ_MODE 2
+#endif
+#ifndef NR_FSWZ_W
+#define NR_FSWZ_W 0
+#endif
+#ifndef NR_SSWZ_MODE
+#define NR_SSWZ_MODE 0
+#endif
+#ifndef NR_FSWZ_H
+#define NR_FSWZ_H 1
+#endif
+template <int MODE, int SW_, int SH>
+__device__ __forceinline__ void xcd_tile(int L, int b, int nx, int ny, int& tx, int& ty) {
+    tx = L % nx;
+    ty = L / nx;
+    if (MODE == 1) {
+        const int SW = SW_ > 0 ? SW_ : nx;
+        const int per = SW * SH;
+        const int ngx = nx / SW;
+        if (per > 1 && nx % SW == 0 && ny % SH == 0 && (ngx * (ny / SH)) % 8 == 0) {
+            const int j = L >> 3, xcd = L & 7;
+            const int grp = (j / per) * 8 + xcd;
+            const int q = j % per;
+            tx = (grp % ngx) * SW + q % SW;
+            ty = (grp / ngx) * SH + q / SW;
+        }
+    } else if (MODE == 2) {
+        if (ny % 8 == 0) {
+            const int j = L >> 3, xcd = L & 7;
+            const int band = (xcd + b) & 7;
+            tx = j % nx;
+            ty = band * (ny >> 3) + j / nx;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// block-wide exclusive scan of one int per thread (NW waves)
+template <int NW = NT / 64>
+__device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds4[wid] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        const int t = lds4[i];
+        base += (i < wid) ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return base + x - v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Texture repacking, carried by other launches: textures [Bt, 3, H, W] (any strides) -> RGBA rows
+// [Bt, HWp, 4] (alpha slot 0) before the sampling (k_face_setup's idle threads), and the [Bt, HWp, 4]
+// gradient accumulator -> [Bt, 3, H, W] after the backward (k_vertex_grad's blocks).  Each block of
+// the carrying grid takes one contiguous slice, so neither needs a launch of its own.
+struct TexPack {
+    const float* __restrict__ tex;
+    long long sb;
+    int sc, sp, HW, HWp;
+    float4* __restrict__ out;  // null: nothing to pack
+    long long n;               // Bt * HWp
+};
+struct TexOut {
+    const float* __restrict__ g4;
+    float* __restrict__ out;   // null: nothing to write
+    int HW, HWp;
+    long long n;               // Bt * HW
+};
+__device__ __forceinline__ void tex_pack_one(const TexPack& pk, long long i) {
+    const long long bt = i / pk.HWp;
+    const int p = (int)(i - bt * pk.HWp);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < pk.HW) {
+        const float* tb = pk.tex + bt * pk.sb + (long long)p * pk.sp;
+        v = make_float4(tb[0], tb[pk.sc], tb[2 * (long long)pk.sc], 0.f);
+    }
+    pk.out[i] = v;
+}
+__device__ __forceinline__ void tex_out_one(const TexOut& to, long long i) {
+    const long long bt = i / to.HW;
+    const int p = (int)(i % to.HW);
+    const float4 v = reinterpret_cast<const float4*>(to.g4)[bt * to.HWp + p];
+    to.out[(bt * 3 + 0) * to.HW + p] = v.x;
+    to.out[(bt * 3 + 1) * to.HW + p] = v.y;
+    to.out[(bt * 3 + 2) * to.HW + p] = v.z;
+}
+// this block's slice [lo, hi) of n items spread over the whole grid
+__device__ __forceinline__ void grid_slice(long long n, long long& lo, long long& hi) {
+    const long long nb = (long long)gridDim.x * gridDim.y;
+    const long long id = (long long)blockIdx.y * gridDim.x + blockIdx.x;
+    const long long chunk = (n + nb - 1) / nb;
+    lo = min(id * chunk, n);
+    hi = min(lo + chunk, n);
+}
+
+}  // namespace

@@ -1,0 +1,429 @@
+// nr_fwd.h -- forward: k_face_setup, k_vertex_normals, k_raster_fwd (face-index map), standalone k_tex_pack
+// Part of nr_raster.hip (one translation unit); see that file and DESIGN.md.
+#pragma once
+
+#pragma clang fp contract(off)
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// k_face_setup: per (face group of 128, item)
+//   GATHER: faces come from vertices[b, faces_idx[f, k]] (rasterize.py:232) and are written to
+//           face_records; otherwise face_records already holds the gathered faces (the
+//           face_index_map_forward_safe entry point receives them that way, rasterize.py:34).
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ vertices, const int32_t* __restrict__ faces_idx,
+                                                    float* __restrict__ face_records, int V, int F, int S,
+                                                    int draw_backside, int2* __restrict__ bbox,
+                                                    uint32_t* __restrict__ mask, int nbx, int nbins, int nwords,
+                                                    const float* __restrict__ vt, long long vt_bstride, int Vt,
+                                                    const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
+                                                    int uv_items, float* __restrict__ fnorm, TexPack pk) {
+    __shared__ int2 s_bb[SETUP_FACES];
+    // the block's face records, assembled per face and then written out coalesced (a record per lane
+    // would store 64-B strided rows); the bin-mask words reuse the space afterwards
+    constexpr int STAGE = SETUP_FACES * FACE_REC;
+    __shared__ __attribute__((aligned(16))) float s_stage[STAGE > SETUP_LDS_WORDS ? STAGE : SETUP_LDS_WORDS];
+    float* s_frec = s_stage;
+    uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_stage);
+    const int b = blockIdx.y;
+    const int f0 = blockIdx.x * SETUP_FACES;
+    const int t = threadIdx.x;
+    if (pk.out && t >= SETUP_FACES) {  // the threads the face phase leaves idle repack the textures
+        long long lo, hi;
+        grid_slice(pk.n, lo, hi);
+        for (long long i = lo + (t - SETUP_FACES); i < hi; i += blockDim.x - SETUP_FACES) tex_pack_one(pk, i);
+    }
+    if (t < SETUP_FACES) {
+        const int f = f0 + t;
+        int2 bb = make_int2(NR_EMPTY_RANGE, NR_EMPTY_RANGE);
+        if (f < F) {
+            float c[9];
+            if (GATHER) {
+                const float* vb = vertices + (long long)b * V * 3;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const int vi = faces_idx[f * 3 + k];
+                    c[3 * k + 0] = vb[vi * 3 + 0];
+                    c[3 * k + 1] = vb[vi * 3 + 1];
+                    c[3 * k + 2] = vb[vi * 3 + 2];
+                }
+                // 16-float record: corners, rcp_nr(z_k), rcp_nr(z_k + 1e-10), range flags (see Face)
+                bool fxyz = true, fzq = true;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    fxyz = fxyz && coord_ok(c[3 * k]) && coord_ok(c[3 * k + 1]) && in_range(c[3 * k + 2], 0x1p-20f, 0x1p20f);
+                    fzq = fzq && in_range(c[3 * k + 2] + 1e-10f, 0x1p-20f, 0x1p20f);
+                }
+#ifdef NR_NO_FASTDIV
+                const int flags = 0;  // timing build: IEEE divisions everywhere
+#else
+                const int flags = (fxyz ? FACE_FAST_XYZ : 0) | (fzq ? FACE_FAST_ZQ : 0);
+#endif
+                float4* rec = reinterpret_cast<float4*>(s_frec + t * FACE_REC);
+                rec[0] = make_float4(c[0], c[1], c[2], c[3]);
+                rec[1] = make_float4(c[4], c[5], c[6], c[7]);
+                rec[2] = make_float4(c[8], rcp_nr(c[2]), rcp_nr(c[5]), rcp_nr(c[8]));
+                rec[3] = make_float4(rcp_nr(c[2] + 1e-10f), rcp_nr(c[5] + 1e-10f), rcp_nr(c[8] + 1e-10f),
+                                     __int_as_float(flags));
+                if (fnorm) {
+                    // face normal cross(v1 - v0, v2 - v1) (rasterize.py:166-170; torch.cross component order)
+                    const float a0 = c[3] - c[0], a1 = c[4] - c[1], a2 = c[5] - c[2];
+                    const float b0 = c[6] - c[3], b1 = c[7] - c[4], b2 = c[8] - c[5];
+                    float* nf = fnorm + ((long long)b * F + f) * 3;
+                    nf[0] = a1 * b2 - a2 * b1;
+                    nf[1] = a2 * b0 - a0 * b2;
+                    nf[2] = a0 * b1 - a1 * b0;
+                }
+            } else {
+                const float* rec = face_records + ((long long)b * F + f) * 9;  // caller's [B, F, 3, 3]
+#pragma unroll
+                for (int k = 0; k < 9; k++) c[k] = rec[k];
+            }
+            const float x0 = c[0], y0 = c[1], x1 = c[3], y1 = c[4], x2 = c[6], y2 = c[7];
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 9; k++) ok = ok && !(c[k] != c[k]);  // NaN faces are never accepted
+            // face-level rejects of .cu:100-104 and .cu:118-121 (pixel independent)
+            if (!draw_backside && (y2 - y0) * (x1 - x0) > (y1 - y0) * (x2 - x0)) ok = false;
+            const float det = x2 * (y0 - y1) + x0 * (y1 - y2) + x1 * (y2 - y0);
+            if ((double)fabsf(det) < 0.00000001) ok = false;
+            if (ok) {
+                int ix0, ix1, iy0, iy1;
+                pix_range(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), S, ix0, ix1);
+                pix_range(fminf(fminf(y0, y1), y2), fmaxf(fmaxf(y0, y1), y2), S, iy0, iy1);
+                if (ix0 <= ix1 && iy0 <= iy1) bb = make_int2(pack_range(ix0, ix1), pack_range(iy0, iy1));
+            }
+            if (face_uv != nullptr && b < uv_items) {
+                const float* vtb = vt + (long long)b * vt_bstride;
+                float uv[6];
+                bool uok = true;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const int ti = faces_t[f * 3 + k];
+                    uv[2 * k + 0] = vtb[(long long)ti * 2 + 0];
+                    uv[2 * k + 1] = vtb[(long long)ti * 2 + 1];
+                }
+#pragma unroll
+                for (int k = 0; k < 6; k++) uok = uok && (uv[k] == 0.f || in_range(uv[k], 0x1p-16f, 0x1p20f));
+                // 8-float texture record: u0 v0 u1 v1 u2 v2, range flag (see sample_texture), pad
+                float4* u = reinterpret_cast<float4*>(face_uv + ((long long)b * F + f) * 8);
+                u[0] = make_float4(uv[0], uv[1], uv[2], uv[3]);
+                u[1] = make_float4(uv[4], uv[5], __int_as_float(uok ? 1 : 0), 0.f);
+            }
+            bbox[(long long)b * F + f] = bb;
+        }
+        s_bb[t] = bb;
+    }
+    __syncthreads();
+    {
+        const int nf = min(SETUP_FACES, F - f0);
+        if (GATHER) {
+            float4* dst = reinterpret_cast<float4*>(face_records + ((long long)b * F + f0) * FACE_REC);
+            const float4* src = reinterpret_cast<const float4*>(s_frec);
+            for (int i = t; i < nf * (FACE_REC / 4); i += blockDim.x) dst[i] = src[i];
+        }
+        __syncthreads();
+    }
+    // coarse-bin bitmask words of this face group
+    const int w0 = blockIdx.x * (SETUP_FACES / 32);
+    const int nw = min(SETUP_FACES / 32, nwords - w0);
+    if (nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS) {
+        // each face sets its bit in the (few) bins its pixel range touches (LDS ds_or), then the
+        // block writes its words out
+        for (int i = t; i < nbins * (SETUP_FACES / 32); i += blockDim.x) s_mask[i] = 0u;
+        __syncthreads();
+        if (t < SETUP_FACES) {
+            const int2 bb = s_bb[t];
+            const int x0 = range_lo(bb.x), x1 = range_hi(bb.x), y0 = range_lo(bb.y), y1 = range_hi(bb.y);
+            if (x0 <= x1 && y0 <= y1) {
+                const int nby = nbins / nbx;
+                for (int by = y0 / COARSE; by <= min(y1 / COARSE, nby - 1); by++)
+                    for (int bx = x0 / COARSE; bx <= min(x1 / COARSE, nbx - 1); bx++)
+                        atomicOr(&s_mask[(by * nbx + bx) * (SETUP_FACES / 32) + (t >> 5)], 1u << (t & 31));
+            }
+        }
+        __syncthreads();
+        for (int p = t; p < nbins * nw; p += blockDim.x) {
+            const int bin = p / nw, wi = p % nw;
+            mask[((long long)b * nbins + bin) * nwords + w0 + wi] = s_mask[bin * (SETUP_FACES / 32) + wi];
+        }
+        return;
+    }
+    for (int p = t; p < nbins * nw; p += blockDim.x) {
+        const int bin = p / nw, wi = p % nw;
+        const int bx0 = (bin % nbx) * COARSE, by0 = (bin / nbx) * COARSE;
+        const int bx1 = bx0 + COARSE - 1, by1 = by0 + COARSE - 1;
+        uint32_t bits = 0;
+#pragma unroll 8
+        for (int j = 0; j < 32; j++) {
+            const int2 bb = s_bb[wi * 32 + j];
+            const bool hit = range_lo(bb.x) <= bx1 && range_hi(bb.x) >= bx0 && range_lo(bb.y) <= by1 &&
+                             range_hi(bb.y) >= by0;
+            bits |= (hit ? 1u : 0u) << j;
+        }
+        mask[((long long)b * nbins + bin) * nwords + w0 + wi] = bits;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// vertex normals (rasterize.py:171-182): u = sum of the normals of the vertex's distinct faces (the
+// reference's one-hot [F, V] matmul), n = u / max(|u|, 1e-12) (F.normalize); stored as (n, |u|)
+__global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t* __restrict__ off,
+                                 const int32_t* __restrict__ vfaces, float* __restrict__ vnorm, int F, int V, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(i / V), v = (int)(i % V);
+    const float* fb = fnorm + (long long)b * F * 3;
+    float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+    for (int e = off[v]; e < off[v + 1]; e++) {
+        const float* nf = fb + vfaces[e] * 3;
+        u0 += nf[0];
+        u1 += nf[1];
+        u2 += nf[2];
+    }
+    const float len = sqrtf((u0 * u0 + u1 * u1) + u2 * u2);
+    const float d = fmaxf(len, 1e-12f);
+    reinterpret_cast<float4*>(vnorm)[i] = make_float4(u0 / d, u1 / d, u2 / d, len);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_raster_fwd<NTF>: one block per 32x32-pixel coarse bin (the bitmask granularity), split into 16
+// 8x8 pixel blocks; NTF / 64 waves, each walking 16 / (NTF / 64) of the 8x8 blocks in turn.
+//   1. the bin's bitmask words are expanded (block scan over popcounts) into the ordered list of
+//      candidate faces;
+//   2. up to FCAP candidates at a time are staged into LDS in ascending face order (one face per
+//      thread, one global load stage);
+//   3. per 8x8 block, the wave ballots which staged faces' float bounding boxes meet the block's
+//      pixel-centre extent (an exact cull: such a face fails .cu:94-97 at every pixel of the block)
+//      and walks the set bits in order (scalar loop), running the reference's per-face test for its
+//      pixel -- every pixel therefore sees its candidate faces in ascending index order, as the
+//      reference's sequential loop does (.cu:82-149), and the per-pixel state stays in registers
+//      across rounds;
+//   shading and the output image are computed by k_shade.
+//   Block sizes (picked per launch, run_face_index): 256 threads = 4 waves, each walking the four 8x8
+//   blocks of a 16x16 quadrant (most per-thread work, least fixed cost per pixel: best when the grid
+//   has many bins of moderate depth, e.g. the headline); 1024 threads = 16 waves, one 8x8 block each
+//   (the bin's walks run 4x wider: small batches, where the grid is a few blocks per CU, and dense
+//   bins -- 300+ faces over one 8x8 block on a 50k-face torus -- no longer serialise on 4 waves).
+//   LDS face record, structure of arrays (float4 i of staged face j at s_face[i * FCAP + j]: the
+//   staging stores are lane-contiguous), 8 x float4:
+//     0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
+//     4: z2 A=x1-x0 B=y1-y0 C=x2-x1 | 5: D=y2-y1 E=x0-x2 F=y0-y2 k0 | 6: k1 k2 1/z0 1/z1 | 7: 1/z2 - - ok
+//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
+constexpr int FREC = 8;  // float4 per staged face
+template <int NTF> struct FwdCfg {
+    static constexpr int NW = NTF / 64;                        // waves
+    static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
+    static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
+    static constexpr int FCAP = NTF >= 1024 ? 256 : 128;       // faces staged per round
+    static constexpr int LDS = FCAP * FREC * 16 + CAND * 4;
+    static_assert(NSUB == 1 || NSUB == 2 || NSUB == 4, "forward block layout");
+    // 8x8 block k of wave w: its origin (ox, oy) in the bin
+    __device__ static __forceinline__ void block_of(int w, int k, int& ox, int& oy) {
+        if (NSUB == 1) {         // 16 waves: wave w owns block (w & 3, w >> 2)
+            ox = (w & 3) * 8;
+            oy = (w >> 2) * 8;
+        } else if (NSUB == 2) {  // 8 waves: a vertical pair of blocks in quadrant w >> 1
+            ox = ((w >> 1) & 1) * 16 + (w & 1) * 8;
+            oy = (w >> 2) * 16 + k * 8;
+        } else {                 // 4 waves: the 16x16 quadrant w, walked as four 8x8 blocks
+            ox = (w & 1) * 16 + (k & 1) * 8;
+            oy = (w >> 1) * 16 + (k >> 1) * 8;
+        }
+    }
+};
+
+// the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel; q0, q1 are
+// the record's first two float4 (loaded ahead by the caller); FST = the SoA stride (FCAP)
+template <int FST>
+__device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1, float xp, float yp, float near, float far,
+                                          float delta, float& depth_min, int& best) {
+#if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 1
+    best += (int)q0.x;  // timing build: no per-pixel test
+    return;
+#endif
+    // The rejections of .cu:94-126 are independent of each other (none changes the state), so their
+    // order is free: the depth-bound reject .cu:124-126 goes first, as it is the cheapest and lets a
+    // whole wave skip a face hidden behind what its pixels already hold.
+    if (depth_min < q1.z) return;
+    // .cu:94-97 (min/max form, exact for non-NaN faces)
+    if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
+    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
+    const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
+    // .cu:107-116
+    const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
+    const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
+    if (c1 * c2 < 0) return;
+    const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
+    if (c2 * c3 < 0) return;
+#if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 2
+    best = __float_as_int(q1.w);  // timing build: no division block
+    return;
+#endif
+    const float4 q6 = e[6 * FST];
+    const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
+    // .cu:130-139
+    float w0 = (yp * q4.w - xp * q5.x) + q5.w;
+    float w1 = (yp * q5.y - xp * q5.z) + q6.x;
+    float w2 = (yp * q4.y - xp * q4.z) + q6.y;
+    const float ws = w0 + w1 + w2;
+    float zp;
+    const float4 q7 = e[7 * FST];
+    if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
+        // face coordinates and depths within [2^-20, 2^20] (or 0) bound every operand below inside
+        // div_nr's exact range (DESIGN.md "Numerics"); 1/z is staged per face
+        const float rs = rcp_nr(ws);
+        w0 = div_nr(w0, ws, rs);
+        w1 = div_nr(w1, ws, rs);
+        w2 = div_nr(w2, ws, rs);
+        const float sum = div_nr(w0, z0, q6.z) + div_nr(w1, z1, q6.w) + div_nr(w2, z2, q7.x);
+        if (in_range(sum, 0x1p-90f, 0x1p90f)) {
+            const float r = rcp_nr(sum);
+            zp = __builtin_fmaf(__builtin_fmaf(-sum, r, 1.f), r, r);  // div_nr(1, sum, r): 1 * r == r
+            zp = __builtin_fmaf(__builtin_fmaf(-sum, zp, 1.f), r, zp);
+        } else {
+            zp = 1.f / sum;
+        }
+    } else {
+        w0 /= ws;
+        w1 /= ws;
+        w2 /= ws;
+        zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
+    }
+    if (zp <= near || far <= zp) return;
+    if (zp <= depth_min - delta) {  // .cu:145-148
+        depth_min = zp;
+        best = __float_as_int(q1.w);
+    }
+}
+
+template <int FST>
+__device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f, int2 bb) {
+    const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
+    const float x2 = c[6], y2 = c[7], z2 = c[8];
+    e[0 * FST] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
+                       fmaxf(fmaxf(y0, y1), y2));
+    e[1 * FST] = make_float4(__int_as_float(bb.x), __int_as_float(bb.y), fminf(fminf(z0, z1), z2), __int_as_float(f));
+    e[2 * FST] = make_float4(x0, y0, x1, y1);
+    e[3 * FST] = make_float4(x2, y2, z0, z1);
+    e[4 * FST] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
+    e[5 * FST] = make_float4(y2 - y1, x0 - x2, y0 - y2, x1 * y2 - x2 * y1);
+    e[6 * FST] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, rcp_nr(z0), rcp_nr(z1));
+    const bool ok = coord_ok(x0) && coord_ok(y0) && coord_ok(x1) && coord_ok(y1) && coord_ok(x2) && coord_ok(y2) &&
+                    in_range(z0, 0x1p-20f, 0x1p20f) && in_range(z1, 0x1p-20f, 0x1p20f) &&
+                    in_range(z2, 0x1p-20f, 0x1p20f);
+    e[7 * FST] = make_float4(rcp_nr(z2), 0.f, 0.f, __int_as_float(ok ? 1 : 0));
+}
+
+#ifndef NR_FWD_WPE
+#define NR_FWD_WPE 8
+#endif
+#ifndef NR_FWD_FORCE_NT
+#define NR_FWD_FORCE_NT 0  // timing builds: 256 / 512 / 1024 threads for every launch
+#endif
+template <int NTF>
+__global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
+                                                  const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
+                                                  int F, Geom g, float near, float far, float delta,
+                                                  int32_t* __restrict__ fim) {
+    using C = FwdCfg<NTF>;
+    constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
+    __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
+    __shared__ int s_scan[C::NW];
+    float4* s_face = reinterpret_cast<float4*>(s_raw);
+    int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
+
+    const int b = blockIdx.y;
+    const int S = g.S;
+    int bin_x, bin_y;
+    xcd_tile<NR_FSWZ_MODE, NR_FSWZ_W, NR_FSWZ_H>(blockIdx.x, b, g.nbx, g.nby, bin_x, bin_y);
+    const int bin = bin_y * g.nbx + bin_x;
+    const int bx0 = bin_x * COARSE;
+    const int by0 = bin_y * COARSE;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wid = t >> 6;
+    float xp[NSUB], yp[NSUB];
+    float depth_min[NSUB];
+    int best[NSUB];
+    float xcl[NSUB], xch[NSUB], ycl[NSUB], ych[NSUB];
+#pragma unroll
+    for (int k = 0; k < NSUB; k++) {
+        int ox, oy;
+        C::block_of(wid, k, ox, oy);
+        xcl[k] = pix_center(bx0 + ox, S);
+        xch[k] = pix_center(bx0 + ox + 7, S);
+        ycl[k] = pix_center(by0 + oy, S);
+        ych[k] = pix_center(by0 + oy + 7, S);
+        xp[k] = pix_center(bx0 + ox + (lane & 7), S);
+        yp[k] = pix_center(by0 + oy + (lane >> 3), S);
+        depth_min[k] = far;
+        best[k] = -1;
+    }
+
+    const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
+    const int2* bbb = bbox + (long long)b * F;
+    const float* frb = face_records + (long long)b * F * rs;
+    int32_t* __restrict__ fimb = fim + (long long)b * S * S;
+
+    for (int wbase = 0; wbase < g.nwords; wbase += NTF) {
+        const int w = wbase + t;
+        const uint32_t bits = (w < g.nwords) ? words[w] : 0u;
+        int total;
+        const int off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
+        for (int cbase = 0; cbase < total; cbase += CAND) {
+            // expand my word's set bits into the ordered candidate list
+            int r = off;
+            for (uint32_t m = bits; m; m &= m - 1, r++) {
+                if (r < cbase) continue;
+                if (r >= cbase + CAND) break;
+                s_cand[r - cbase] = w * 32 + __builtin_ctz(m);
+            }
+            __syncthreads();
+            const int nc = min(CAND, total - cbase);
+            for (int j0 = 0; j0 < nc; j0 += FCAP) {
+                const int n = min(FCAP, nc - j0);
+                if (t < n) {
+                    const int f = s_cand[j0 + t];
+                    stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < NSUB; k++) {
+                    const float xc0 = xcl[k], xc1 = xch[k], yc0 = ycl[k], yc1 = ych[k];
+                    for (int c0 = 0; c0 < n; c0 += 64) {
+                        bool hit = false;
+                        if (c0 + lane < n) {
+                            const float4 q0 = s_face[c0 + lane];
+                            hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
+                        }
+                        // faces touching this wave's pixels, walked in ascending order
+                        for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
+                            const float4* e = s_face + (c0 + __builtin_ctzll(m));
+                            const float4 q0 = e[0], q1 = e[FCAP];
+                            face_test<FCAP>(e, q0, q1, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+
+#pragma unroll
+    for (int k = 0; k < NSUB; k++) {
+        int ox, oy;
+        C::block_of(wid, k, ox, oy);
+        const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
+        if (px < S && py < S) fimb[py * S + px] = best[k];
+    }
+}
+
+
+// textures [Bt, 3, H, W] (any strides) -> RGBA rows [Bt, HWp, 4] (alpha slot 0), read by the sampling
+__global__ void k_tex_pack(TexPack pk) {  // standalone form (no face setup to carry it)
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < pk.n) tex_pack_one(pk, i);
+}
+
+}  // namespace

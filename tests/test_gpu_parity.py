@@ -616,6 +616,37 @@ def test_backgrounds_vs_oracle(oracle_mod, dev, aa, size, lit):
         close_grads(out["gpu"][i], out["cpu"][i], "grad " + what)
 
 
+@pytest.mark.parametrize("per_item,ts", [(False, 2), (True, 8)])
+def test_texture_repack_and_transpose_paths_vs_oracle(oracle_mod, dev, per_item, ts):
+    """The texture repack and the texture-gradient transpose run inside k_face_setup /
+    k_vertex_grad when they are small (a shared 36x36 atlas here) and as launches of their own when
+    they are not (per-item 144x144 atlases, whose 8x8 texel tiles also exceed the backward's 4x4
+    face window): images, vertex and texture gradients against the CPU oracle either way."""
+    B = 2
+    proj, f = _ico_batch(2, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=ts)
+    shape = ((B,) if per_item else (1,)) + tex.shape
+    tex = torch.rand(shape, generator=torch.Generator().manual_seed(21))
+    g = torch.randn((B, 5, 48, 48), generator=torch.Generator().manual_seed(22))
+    out = {}
+    for where in ("gpu", "cpu"):
+        d = dev if where == "gpu" else torch.device("cpu")
+        pv = proj.to(d).clone().requires_grad_(True)
+        tx = tex.to(d).clone().requires_grad_(True)
+        texb = tx if per_item else tx.expand(B, -1, -1, -1)
+        vts = torch.as_tensor(vt, device=d)[None].expand(B, -1, -1)
+        if where == "gpu":
+            params = nr.RasterizeParam(vertices_textures=vts, faces_textures=torch.as_tensor(ft, device=d), textures=texb)
+            img = nrr.rasterize_core(pv, torch.as_tensor(f, device=d), params, nr.RasterizeHyperparam(image_size=48))
+        else:
+            img = oracle_mod.rasterize_core(pv, f, image_size=48, vertices_textures=vts, faces_textures=ft, textures=texb)
+        img.backward(g.to(d))
+        out[where] = (img.detach().cpu(), pv.grad.cpu(), tx.grad.cpu())
+    close_images(out["gpu"][0], out["cpu"][0], "images")
+    close_grads(out["gpu"][1], out["cpu"][1], "grad vertices")
+    close_grads(out["gpu"][2], out["cpu"][2], "grad textures")
+
+
 def test_background_color_is_black(dev):
     """background_color: the reference computes zeros * colour (rasterize.py:208-214), a black
     background; the parameter object gets the backgrounds tensor, as the reference sets it."""

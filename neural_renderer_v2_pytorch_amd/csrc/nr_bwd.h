@@ -435,7 +435,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         if (!(NR_ABLATE & 16) && h_in) {
             const int hf = fimb[hpy * S + hpx];
             Face ff = empty_face();
-            if (hf >= 0) ff = load_face_rec(frb + hf * FACE_REC);
+            if (hf >= 0 && shade_needs_face(sh)) ff = load_face_rec(frb + hf * FACE_REC);
             shade_pixel(sh, b, hf, ff, hpx, hpy, S, hI);
             upstream_grad(a, gimb, C, hpy, hpx, S, hG);
         }

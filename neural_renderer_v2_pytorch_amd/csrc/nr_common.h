@@ -426,12 +426,15 @@ __device__ __forceinline__ void background(const Shade& sh, int b, int x, int y,
 
 // All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth), written
 // to compile-time slots of out[MAXC] (runtime-indexed register arrays would spill to scratch).
+__device__ __forceinline__ bool shade_needs_face(const Shade& sh) { return (sh.draw & (NR_DRAW_RGB | NR_DRAW_DEPTH)) != 0; }
 __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, int x, int y, int S,
                                             float* out) {
     const bool R = (sh.draw & NR_DRAW_RGB) != 0, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
     const float xp = pix_center(x, S), yp = pix_center(y, S);
     float r = 0.f, gg = 0.f, bb = 0.f, sil = 0.f, dep = 0.f;
-    if (fi >= 0) {
+    if (fi >= 0) sil = 1.f;
+    // the weights (and the face record) only feed rgb and depth: a silhouettes-only render skips them
+    if (fi >= 0 && shade_needs_face(sh)) {
         float w[3];
         const bool wfast = face_weights(xp, yp, f, w);
         if (R) {
@@ -450,7 +453,6 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
                 bb = bb * cw[2];
             }
         }
-        sil = 1.f;
         if (sh.draw & NR_DRAW_DEPTH) dep = depth_value(f, w, wfast);
     }
     if (R && sh.bg) {  // fg * rgb + (1 - fg) * bg (chainer rasterize.py:576)

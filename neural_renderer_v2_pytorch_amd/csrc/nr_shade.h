@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
         const int y = S - 1 - oi, x = S - 1 - oj;
         const int fi = fb[y * S + x];
         Face f = empty_face();
-        if (fi >= 0) f = load_face_rec(frb + fi * FACE_REC);
+        if (fi >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fi * FACE_REC);
         float v[MAXC];
         shade_pixel(sh, b, fi, f, x, y, S, v);
 #pragma unroll
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         Face f = empty_face();
-        if (fis[q] >= 0) f = load_face_rec(frb + fis[q] * FACE_REC);
+        if (fis[q] >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fis[q] * FACE_REC);
         shade_pixel(sh, b, fis[q], f, xs[q], ys[q], S, v[q]);
     }
 #pragma unroll
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
     }
     const int fi = fb[y * S + x];
     Face f = empty_face();
-    if (fi >= 0) f = load_face_rec(frb + fi * FACE_REC);
+    if (fi >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fi * FACE_REC);
     float v[MAXC];
     shade_pixel(sh, b, fi, f, x, y, S, v);
     const bool live = o < s * s;

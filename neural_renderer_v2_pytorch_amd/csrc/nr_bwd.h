@@ -158,6 +158,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     const int C = sh.C;
     const bool rgb = (sh.draw & NR_DRAW_RGB) != 0;
     const bool want_tex = rgb && a.grad_tex4 != nullptr;
+    const bool wlate = !rgb && !(sh.draw & NR_DRAW_DEPTH);  // silhouettes only (uniform)
     int tile_x, tile_y;
     xcd_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(blockIdx.x, b, (S + TW - 1) / TW, (S + BH - 1) / BH, tile_x, tile_y);
     const int tx0 = tile_x * TW;
@@ -256,6 +257,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         if (q.fi < 0) continue;
         const float yp = pix_center(py, S);
         const float* G = G2[k];
+        if (wlate) {  // silhouettes only: I is (fim >= 0); the weights after the stencil, where needed
+            I2[k][0] = 1.f;
+            continue;
+        }
         Face f = load_face_rec(frb + q.fi * FACE_REC);
 #ifndef NR_BWD_FASTDIV
         f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
@@ -454,7 +459,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     float gF[NPX][9];
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
-        const BwdPix& q = P[k];
+        BwdPix& q = P[k];
 #pragma unroll
         for (int j = 0; j < 9; j++) gF[k][j] = 0.f;
         if (q.fi < 0) continue;
@@ -477,6 +482,15 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
         }
         const float gy = (NR_ABLATE & 64) ? Ip[0] : stencil(a, Im, I0, Ip, Gm, G0, Gp, py, S, C);
+        if (wlate && (gx != 0.f || gy != 0.f)) {
+            // silhouettes only: the stencil is zero away from silhouette edges, so only these pixels
+            // fetch their face and weights (the same computation as in step 1)
+            Face f = load_face_rec(frb + q.fi * FACE_REC);
+#ifndef NR_BWD_FASTDIV
+            f.flags = 0;
+#endif
+            face_weights(xp, pix_center(py, S), f, q.w);
+        }
         // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
 #pragma unroll
         for (int j = 0; j < 3; j++) {
@@ -522,7 +536,16 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     float* __restrict__ gNb = LIT ? a.grad_normals + (long long)b * a.F * 9 : nullptr;
     // the second pixel's state (NPX == 1: none, never active)
     const int fi1 = NPX > 1 ? P[NPX - 1].fi : -1, wx1 = NPX > 1 ? P[NPX - 1].wx : 0, wy1 = NPX > 1 ? P[NPX - 1].wy : 0;
-    const bool act0 = P[0].fi >= 0, act1 = fi1 >= 0;
+    // silhouettes only: a pixel whose face gradient is all zero (away from silhouette edges, the
+    // stencil is zero) adds nothing, so it stays out of the per-face gather
+    bool nz[NPX];
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        nz[k] = !wlate;
+#pragma unroll
+        for (int j = 0; j < 9; j++) nz[k] = nz[k] || gF[k][j] != 0.f;
+    }
+    const bool act0 = P[0].fi >= 0 && nz[0], act1 = fi1 >= 0 && nz[NPX - 1];
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
     // texel lanes: consecutive faces with the same texel window (e.g. every face of a flat-colour
     // material samples one 2x2 atlas patch, load_obj.py:84-94) accumulate into `pend` and flush once

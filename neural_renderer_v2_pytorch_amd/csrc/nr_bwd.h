@@ -46,6 +46,9 @@ static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 #ifndef NR_ABLATE
 #define NR_ABLATE 0
 #endif
+#ifndef NR_BWD_SKIP_ZERO
+#define NR_BWD_SKIP_ZERO 0  // 1: any all-zero pixel skips the gather (costs the headline ~0.5 %); 0: silhouettes-only renders only
+#endif
 #ifndef NR_HALO_EARLY
 #define NR_HALO_EARLY 1
 #endif
@@ -136,14 +139,14 @@ struct BwdPix {
     float gn[3];       // lights: dL/d(smooth normal)
 };
 
-// FEAT: 1 = lights, 2 = backgrounds (separate instantiations keep the plain path lean)
+// FEAT: 1 = lights, 2 = backgrounds, 4 = silhouettes only (separate instantiations keep the plain path lean)
 // NPX: pixels per lane (2: 256 threads, a wave = 16x8 pixels; 1: 512 threads, a wave = 16x4 pixels)
 #ifndef NR_BWD_WPE1
 #define NR_BWD_WPE1 6
 #endif
 template <int FEAT, int NPX>
 __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? NR_BWD_WPE1 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
-    constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0;
+    constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0, SILO = (FEAT & 4) != 0;
     // features this instantiation does not have become compile-time constants (the shared
     // shade_pixel then carries no light / background code or arguments)
     Shade sh = sh_in;
@@ -156,9 +159,9 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     const int b = blockIdx.y;
     const int S = g.S;
     const int C = sh.C;
-    const bool rgb = (sh.draw & NR_DRAW_RGB) != 0;
+    const bool rgb = !SILO && (sh.draw & NR_DRAW_RGB) != 0;
     const bool want_tex = rgb && a.grad_tex4 != nullptr;
-    const bool wlate = !rgb && !(sh.draw & NR_DRAW_DEPTH);  // silhouettes only (uniform)
+    constexpr bool wlate = SILO;  // silhouettes only: weights after the stencil, sparse gather
     int tile_x, tile_y;
     xcd_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(blockIdx.x, b, (S + TW - 1) / TW, (S + BH - 1) / BH, tile_x, tile_y);
     const int tx0 = tile_x * TW;
@@ -536,14 +539,20 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     float* __restrict__ gNb = LIT ? a.grad_normals + (long long)b * a.F * 9 : nullptr;
     // the second pixel's state (NPX == 1: none, never active)
     const int fi1 = NPX > 1 ? P[NPX - 1].fi : -1, wx1 = NPX > 1 ? P[NPX - 1].wx : 0, wy1 = NPX > 1 ? P[NPX - 1].wy : 0;
-    // silhouettes only: a pixel whose face gradient is all zero (away from silhouette edges, the
-    // stencil is zero) adds nothing, so it stays out of the per-face gather
+    // a pixel whose every contribution is zero stays out of the per-face gather (exact: it would add
+    // zeros): silhouettes away from silhouette edges, where the stencil is zero, or any pixel whose
+    // upstream gradient is zero (a loss on some channels or regions only)
     bool nz[NPX];
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
-        nz[k] = !wlate;
+        bool v = !NR_BWD_SKIP_ZERO && !wlate;
+        if (NR_BWD_SKIP_ZERO) {
+            v = want_tex && P[k].pos >= 0 && (P[k].grgb[0] != 0.f || P[k].grgb[1] != 0.f || P[k].grgb[2] != 0.f);
+            if (LIT) v = v || P[k].gn[0] != 0.f || P[k].gn[1] != 0.f || P[k].gn[2] != 0.f;
+        }
 #pragma unroll
-        for (int j = 0; j < 9; j++) nz[k] = nz[k] || gF[k][j] != 0.f;
+        for (int j = 0; j < 9; j++) v = v || gF[k][j] != 0.f;
+        nz[k] = v;
     }
     const bool act0 = P[0].fi >= 0 && nz[0], act1 = fi1 >= 0 && nz[NPX - 1];
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);

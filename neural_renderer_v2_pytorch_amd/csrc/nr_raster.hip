@@ -307,11 +307,13 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     {
         ProfScope _p(P_BWD, st);
         const dim3 grid(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size);
-        switch ((lit ? 1 : 0) | (sh.bg ? 2 : 0)) {
+        const bool silo = !(a->draw_flags & (NR_DRAW_RGB | NR_DRAW_DEPTH));  // lights / backgrounds need rgb
+        switch ((lit ? 1 : 0) | (sh.bg ? 2 : 0) | (silo ? 4 : 0)) {
             case 0: launch_bwd<0>(grid, st, ba, g, sh); break;
             case 1: launch_bwd<1>(grid, st, ba, g, sh); break;
             case 2: launch_bwd<2>(grid, st, ba, g, sh); break;
-            default: launch_bwd<3>(grid, st, ba, g, sh); break;
+            case 3: launch_bwd<3>(grid, st, ba, g, sh); break;
+            default: launch_bwd<4>(grid, st, ba, g, sh); break;
         }
     }
     e = check_launch("k_raster_bwd");

@@ -647,6 +647,35 @@ def test_texture_repack_and_transpose_paths_vs_oracle(oracle_mod, dev, per_item,
     close_grads(out["gpu"][2], out["cpu"][2], "grad textures")
 
 
+def test_partial_upstream_gradient_vs_oracle(oracle_mod, dev):
+    """A loss on some channels and regions only (zero upstream gradient elsewhere): the backward
+    leaves zero-contribution pixels out of its per-face gather; gradients against the oracle."""
+    B = 2
+    proj, f = _ico_batch(2, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.rand(tex.shape, generator=torch.Generator().manual_seed(31))
+    g = torch.randn((B, 5, 40, 40), generator=torch.Generator().manual_seed(32))
+    g[:, 0:3] = 0.0          # no loss on rgb
+    g[:, :, :, 20:] = 0.0    # nor on the right half
+    out = {}
+    for where in ("gpu", "cpu"):
+        d = dev if where == "gpu" else torch.device("cpu")
+        pv = proj.to(d).clone().requires_grad_(True)
+        tx = tex.to(d).clone().requires_grad_(True)
+        vts = torch.as_tensor(vt, device=d)[None].expand(B, -1, -1)
+        if where == "gpu":
+            params = nr.RasterizeParam(vertices_textures=vts, faces_textures=torch.as_tensor(ft, device=d),
+                                       textures=tx[None].expand(B, -1, -1, -1))
+            img = nrr.rasterize_core(pv, torch.as_tensor(f, device=d), params, nr.RasterizeHyperparam(image_size=40))
+        else:
+            img = oracle_mod.rasterize_core(pv, f, image_size=40, vertices_textures=vts, faces_textures=ft,
+                                            textures=tx[None].expand(B, -1, -1, -1))
+        img.backward(g.to(d))
+        out[where] = (pv.grad.cpu(), tx.grad.cpu())
+    close_grads(out["gpu"][0], out["cpu"][0], "grad vertices")
+    close_grads(out["gpu"][1], out["cpu"][1], "grad textures")
+
+
 def test_background_color_is_black(dev):
     """background_color: the reference computes zeros * colour (rasterize.py:208-214), a black
     background; the parameter object gets the backgrounds tensor, as the reference sets it."""

@@ -497,7 +497,7 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
 #define NR_FSWZ_W 0
 #endif
 #ifndef NR_SSWZ_MODE
-#define NR_SSWZ_MODE 0
+#define NR_SSWZ_MODE 2  // k_shade: bands of its 1-D block range per XCD (v23: 0.104 -> 0.100 ms on the headline)
 #endif
 #ifndef NR_FSWZ_H
 #define NR_FSWZ_H 1

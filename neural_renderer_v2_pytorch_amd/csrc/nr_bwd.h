@@ -659,6 +659,9 @@ void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, con
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
 }
 
+#ifndef NR_VGRAD_UNROLL
+#define NR_VGRAD_UNROLL 4
+#endif
 // gathered-face gradient -> vertex gradient: gV[b, v] = sum over (f, k) with faces[f, k] = v of gF[b, f, k]
 // (the index backward of rasterize.py:232), through a CSR adjacency built once per faces tensor.
 __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __restrict__ off,
@@ -674,7 +677,32 @@ __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __res
     const int b = (int)(i / V), v = (int)(i % V);
     const float* base = gF + (long long)b * F * 9;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int e = off[v]; e < off[v + 1]; e++) {
+    const int e0 = off[v], e1 = off[v + 1];
+#if NR_VGRAD_UNROLL > 1
+    // entries read NR_VGRAD_UNROLL at a time (their row loads in flight together); the sums keep the
+    // CSR order
+    int e = e0;
+    for (; e + NR_VGRAD_UNROLL <= e1; e += NR_VGRAD_UNROLL) {
+        int en[NR_VGRAD_UNROLL];
+#pragma unroll
+        for (int u = 0; u < NR_VGRAD_UNROLL; u++) en[u] = ent[e + u];
+        float3 rv[NR_VGRAD_UNROLL];
+#pragma unroll
+        for (int u = 0; u < NR_VGRAD_UNROLL; u++) {
+            const float* r = base + (long long)en[u] * 3;
+            rv[u] = make_float3(r[0], r[1], r[2]);
+        }
+#pragma unroll
+        for (int u = 0; u < NR_VGRAD_UNROLL; u++) {
+            s0 += rv[u].x;
+            s1 += rv[u].y;
+            s2 += rv[u].z;
+        }
+    }
+    for (; e < e1; e++) {
+#else
+    for (int e = e0; e < e1; e++) {
+#endif
         const float* r = base + (long long)ent[e] * 3;  // entry = 3 f + k
         s0 += r[0];
         s1 += r[1];

@@ -425,7 +425,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     const bool h_in = t < NHALO && hpy >= 0 && hpy < S && hpx >= 0 && hpx < S;
     if (a.halo) {
         __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMA halo loads have landed
+        // each lane t < NHALO moves the halo values it loaded itself (s_hI/s_hG slot t), so its own
+        // vmcnt wait is enough: no barrier before the move (NR_HALO_BARRIER restores one)
+#ifdef NR_HALO_BARRIER
         __syncthreads();
+#endif
         if (t < NHALO) {
             const int hl = hy * HW_ + hx;
 #pragma unroll

@@ -385,9 +385,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         }
         if ((sh.draw & NR_DRAW_DEPTH) && !(NR_ABLATE & 256)) {
             dep = depth_value(f, w, wfast);
-            // depth channel gradient reloaded (cache hit) rather than a runtime-indexed register array
+            // depth channel gradient: selected from the registers with compile-time indices (a
+            // runtime-indexed register array would go to scratch)
             const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
-            const float gd = upstream_one(a, gimb, py, px, S, dc);
+            const float gd = dc == 4 ? G[4] : dc == 3 ? G[3] : dc == 1 ? G[1] : G[0];
             const float g_s = -gd * (dep * dep);
             const float z[3] = {f.z0, f.z1, f.z2};
 #pragma unroll

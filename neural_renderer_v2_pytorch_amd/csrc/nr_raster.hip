@@ -262,7 +262,16 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
                           void* workspace, size_t workspace_bytes, void* stream) {
     int e = validate_raster(a, false);
     if (e) return e;
-    if (a->batch_size == 0) return NR_OK;
+    if (a->batch_size == 0) {
+        // an empty batch still owes the caller its batch-shared gradient: a shared texture
+        // (tex_stride_b == 0: one item) gets zeros; per-item textures and backgrounds have no items
+        if ((a->draw_flags & NR_DRAW_RGB) && grad_textures && !a->tex_stride_b) {
+            const size_t n = (size_t)3 * a->tex_height * a->tex_width * sizeof(float);
+            if (n && hipMemsetAsync(grad_textures, 0, n, (hipStream_t)stream) != hipSuccess)
+                return check_launch("hipMemsetAsync");
+        }
+        return NR_OK;
+    }
     if (!grad_images || !grad_vertices) return fail(NR_ERR_ARGS, "null gradient buffers");
     if (a->num_faces > 0 && (!a->vertex_offsets || !a->vertex_faces))
         return fail(NR_ERR_ARGS, "missing vertex adjacency (vertex_offsets / vertex_faces)");

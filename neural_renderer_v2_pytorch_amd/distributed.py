@@ -16,9 +16,11 @@ import torch
 import torch.distributed as dist
 
 
-def world():
+def world(group=None):
+    """(rank, world size) within `group` (the default group when None); (0, 1) without a
+    process group."""
     if dist.is_available() and dist.is_initialized():
-        return dist.get_rank(), dist.get_world_size()
+        return dist.get_rank(group), dist.get_world_size(group)
     return 0, 1
 
 
@@ -40,9 +42,9 @@ def shard(tensor, rank=None, world_size=None, dim=0):
 def gather_images(local, batch_size=None, group=None):
     """All-gather batch shards [b_r, ...] into the full batch [B, ...] on every rank.
 
-    Uneven shards (B not divisible by the world size) are padded to the largest shard for the
-    collective and trimmed afterwards."""
-    rank, ws = world()
+    Uneven shards (B not divisible by the group size) are padded to the largest shard for the
+    collective and trimmed afterwards.  Shards are ordered by rank within `group`."""
+    rank, ws = world(group)
     if ws == 1:
         return local
     if batch_size is None:
@@ -64,10 +66,17 @@ def gather_images(local, batch_size=None, group=None):
 
 
 def allreduce_shared_grads(params, group=None):
-    """Sum the gradients of parameters shared by every rank's items (in place)."""
-    _, ws = world()
+    """Sum the gradients of parameters shared by every rank's items (in place).
+
+    Every rank issues the same collectives in the same order: a parameter whose .grad is None on
+    this rank (an empty shard, or a branch this rank did not take) contributes zeros, and its
+    .grad is materialised, so no rank skips an all_reduce the others enter."""
+    _, ws = world(group)
     if ws == 1:
         return
     for p in params:
-        if p is not None and p.grad is not None:
-            dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=group)
+        if p is None:
+            continue
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=group)

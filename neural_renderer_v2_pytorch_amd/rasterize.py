@@ -136,12 +136,15 @@ def _faces_i32(faces, device, bound, what):
     reuse = f.dtype == torch.int32 and f.is_contiguous() and f.device == device
     f = f.to(device=device, dtype=torch.int32).contiguous()
     key = (f.data_ptr(), f._version, f.shape[0], bound)
-    if f.numel() and not (reuse and _faces_checked.get(what) == key):
+    hit = _faces_checked.get(what)
+    if f.numel() and not (reuse and hit is not None and hit[0] == key):
         lo, hi = int(f.min()), int(f.max())
         if lo < 0 or hi >= bound:
             raise IndexError("%s index out of range [0, %d): min %d max %d" % (what, bound, lo, hi))
         if reuse:
-            _faces_checked[what] = key
+            # the entry holds the tensor: its storage, hence the address in the key, cannot be
+            # freed and reused by another tensor while the entry is live
+            _faces_checked[what] = (key, f)
     return f
 
 
@@ -296,6 +299,17 @@ class Rasterize(torch.autograd.Function):
         B = cfg.B
         S = cfg.image_size * (2 if cfg.aa else 1)
         L = _lib.lib()
+        if B == 0:
+            # an empty shard (distributed.shard with B < world size): nothing to draw, and the
+            # backward returns zero gradients for the batch-shared inputs
+            ctx.cfg = cfg
+            ctx.dev = dev
+            ctx.shapes = (textures.shape, ctx.vt_shape, None if light_recs is None else light_recs.shape,
+                          None if backgrounds is None else backgrounds.shape)
+            fim = torch.empty((0, S, S), dtype=torch.int32, device=dev)
+            ctx.mark_non_differentiable(fim)
+            ctx.set_materialize_grads(False)
+            return torch.empty((0, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev), fim
         fim = torch.empty((B, S, S), dtype=torch.int32, device=dev)
         face_records = torch.empty((B, cfg.F, 16), dtype=torch.float32, device=dev)  # nr_raster.h NrRasterArgs
         rgb = bool(cfg.flags & _lib.NR_DRAW_RGB)
@@ -340,6 +354,12 @@ class Rasterize(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_images, _grad_fim):
         cfg = ctx.cfg
+        if cfg.B == 0:
+            tshape, vtshape, lshape, bshape = ctx.shapes
+            dev = ctx.dev
+            z = (lambda shp, i: torch.zeros(shp, dtype=torch.float32, device=dev) if ctx.needs_input_grad[i] else None)
+            return (z((0, cfg.V, 3), 0), z(tshape, 1), z(vtshape, 2), None, None,
+                    z(bshape, 5) if bshape is not None else None, z(lshape, 6) if lshape is not None else None, None)
         vertices, textures, vt, faces, ft, face_records, face_uv, fim, halo, backgrounds = ctx.saved_tensors
         if vt.ndim == 3 and vt.shape[0] == 1 and cfg.B > 1:
             vt = vt.expand(cfg.B, -1, -1)
@@ -467,6 +487,11 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
         H, W = tex.shape[2], tex.shape[3]
         if tex.shape[0] > 1 and tex.stride(0) != 0 and tex.stride(2) != W * tex.stride(3):
             tex = tex.contiguous()
+        if tex.shape[0] > 1 and tex.stride(0) == 0 and tex.requires_grad and tex.grad_fn is None:
+            # a batch-expanded view that is itself the gradient leaf (expand(...).requires_grad_()):
+            # autograd gives such a leaf one gradient per item (t.grad[b] = item b's share), as the
+            # reference fills it, so it is rendered as B per-item textures (a copy, this case only)
+            tex = tex.contiguous()
         cfg.tex_hw = (H, W)
         cfg.tex_shared = tex.shape[0] == 1 or tex.stride(0) == 0
         if cfg.tex_shared:
@@ -474,7 +499,12 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
             # reference tests' idiom) is handed to the Function as its [3, H, W] source so that the
             # texture gradient is returned once, not B times through expand's backward.
             item = tex[0]
+            # the view's base takes the gradient in place of the view only when the gradient reaches
+            # the caller's leaf through it: the view is not itself a leaf that requires grad
+            # (that case was made per-item above), so its grad_fn, if any, is expand's of `base`
             base = tex._base if tex._is_view() else None
+            if base is not None and tex.requires_grad and not base.requires_grad:
+                base = None
             if (base is not None and base.numel() == 3 * H * W and base.is_contiguous()
                     and item.is_contiguous() and item.data_ptr() == base.data_ptr()):
                 tex = base

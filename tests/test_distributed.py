@@ -97,3 +97,43 @@ def test_gloo_world2_matches_full_batch(tmp_path, oracle_mod, batch):
         assert np.array_equal(got["images_known"], images.detach().numpy())
         np.testing.assert_allclose(got["grad"], base.grad.numpy(), rtol=1e-5, atol=1e-6)
     assert float(base.grad.abs().sum()) > 0
+
+
+def _group_worker(rank, world_size, port, out_dir):
+    """Subgroup collectives and a rank with no gradient (distributed.py: world(group),
+    allreduce_shared_grads' zero contribution)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        group = dist.new_group([0, 2])  # every rank creates it, as torch requires
+        res = {}
+        if rank in (0, 2):
+            grank, gws = ndist.world(group)
+            assert gws == 2 and grank == (0 if rank == 0 else 1)
+            batch = 5
+            lo, hi = ndist.shard_range(batch, grank, gws)
+            local = torch.arange(lo, hi, dtype=torch.float32)[:, None].repeat(1, 3)
+            res["gathered"] = ndist.gather_images(local, group=group).numpy()
+            res["gathered_known"] = ndist.gather_images(local, batch_size=batch, group=group).numpy()
+        # a shared parameter whose grad is None on rank 1 (an empty shard): every rank still
+        # enters the all_reduce and the sum is that of the ranks that had a gradient
+        p = torch.zeros(4, requires_grad=True)
+        if rank != 1:
+            (p * float(rank + 1)).sum().backward()
+        ndist.allreduce_shared_grads([p])
+        res["grad"] = p.grad.numpy()
+        np.savez(os.path.join(out_dir, "g%d.npz" % rank), **res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_subgroup_and_missing_grad(tmp_path):
+    mp.spawn(_group_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
+    want = np.repeat(np.arange(5, dtype=np.float32)[:, None], 3, 1)
+    for r in range(3):
+        got = np.load(str(tmp_path / ("g%d.npz" % r)))
+        np.testing.assert_array_equal(got["grad"], np.full(4, 1.0 + 3.0, np.float32))
+        if r != 1:
+            np.testing.assert_array_equal(got["gathered"], want)
+            np.testing.assert_array_equal(got["gathered_known"], want)

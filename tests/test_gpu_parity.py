@@ -403,6 +403,59 @@ def test_empty_and_degenerate(dev):
         nr.rasterize_silhouettes(v, torch.as_tensor([[0, 1, 7]]), nr.RasterizeParam(), hp)
 
 
+def test_empty_batch_textured(dev):
+    """An rgb render of an empty shard (B=0): empty images; the batch-shared texture and the
+    shared vertices_textures get zero gradients (nr_rasterize_backward's B == 0 path)."""
+    vt, ft, tex = nr.create_textures(4, texture_size=2)
+    tex_leaf = torch.as_tensor(tex, device=dev).requires_grad_(True)
+    vt_leaf = torch.as_tensor(vt, device=dev).requires_grad_(True)
+    v = torch.zeros((0, 4, 3), device=dev, requires_grad=True)
+    f = torch.as_tensor([[0, 1, 2], [1, 2, 3], [0, 2, 3], [0, 1, 3]], device=dev)
+    params = nr.RasterizeParam(vertices_textures=vt_leaf[None].expand(0, -1, -1),
+                               faces_textures=torch.as_tensor(ft, device=dev),
+                               textures=tex_leaf[None].expand(0, *tex_leaf.shape))
+    hp = nr.RasterizeHyperparam(image_size=16)
+    img = nr.rasterize_rgba(v, f, params, hp)
+    assert img.shape == (0, 4, 16, 16)
+    img.sum().backward()
+    assert v.grad is not None and v.grad.shape == (0, 4, 3)
+    assert tex_leaf.grad is not None and float(tex_leaf.grad.abs().max()) == 0
+
+
+def test_expanded_texture_leaf_gets_per_item_grads(golden, dev):
+    """textures = tex[None].expand(B, ...).requires_grad_() (the reference tests' idiom with the
+    expanded view as the leaf): autograd gives that leaf one gradient per item, as the reference
+    fills it.  Their sum is the shared-texture golden gradient, and item b's share is what item b
+    rendered alone gives its texture."""
+    d = golden("teapot_rgbsd_aa")
+    assert int(d["shared_textures"])
+    B = d["proj"].shape[0]
+    proj = torch.as_tensor(d["proj"], device=dev)
+    faces = torch.as_tensor(d["faces"], device=dev)
+    ft = torch.as_tensor(d["faces_textures"], device=dev)
+    g = torch.as_tensor(d["grad_up"], device=dev)
+    tex = torch.as_tensor(d["textures"], device=dev)[None].expand(B, *d["textures"].shape).requires_grad_()
+    assert tex.grad_fn is None and tex.stride(0) == 0
+    vt = torch.as_tensor(d["vertices_textures"], device=dev)[None]
+
+    def hp():
+        return nr.RasterizeHyperparam(image_size=int(d["image_size"]), anti_aliasing=bool(d["anti_aliasing"]),
+                                      draw_backside=bool(d["draw_backside"]), **flags_of("teapot_rgbsd_aa"))
+
+    params = nr.RasterizeParam(vertices_textures=vt.expand(B, -1, -1), faces_textures=ft, textures=tex)
+    img = nrr.rasterize_core(proj, faces, params, hp())
+    close_images(img, d["images"], "expanded-leaf images")
+    img.backward(g)
+    assert tex.grad is not None and tex.grad.shape == tex.shape
+    close_grads(tex.grad.sum(0), d["grad_textures"], "expanded-leaf grad textures (sum over items)")
+    for b in range(B):
+        t1 = torch.as_tensor(d["textures"], device=dev)[None].requires_grad_()
+        one = nrr.rasterize_core(proj[b:b + 1], faces, nr.RasterizeParam(vertices_textures=vt, faces_textures=ft,
+                                                                          textures=t1), hp())
+        one.backward(g[b:b + 1])
+        close_grads(tex.grad[b], t1.grad[0], "expanded-leaf grad textures, item %d" % b)
+
+
 def test_reference_binding_module(golden, dev):
     """neural_renderer_v2_pytorch_amd.rasterize_cuda, driven the way the reference's own
     rasterize.py:27-38 and :67-77 drive its pybind module (flat -1-filled index buffer, zeroed

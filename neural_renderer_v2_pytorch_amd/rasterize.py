@@ -498,6 +498,11 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
             # one texture for every item.  A batch-expanded view (tex[None].expand(B, ...), the
             # reference tests' idiom) is handed to the Function as its [3, H, W] source so that the
             # texture gradient is returned once, not B times through expand's backward.
+            if tex.shape[0] == 0:
+                # an empty batch (B = 0) of an expanded view: its source takes the zero gradient
+                base = tex._base if tex._is_view() else None
+                tex = (base.reshape(1, 3, H, W) if base is not None and base.numel() == 3 * H * W
+                       else torch.zeros((1, 3, H, W), dtype=torch.float32, device=dev))
             item = tex[0]
             # the view's base takes the gradient in place of the view only when the gradient reaches
             # the caller's leaf through it: the view is not itself a leaf that requires grad

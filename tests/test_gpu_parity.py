@@ -182,7 +182,7 @@ def test_backward_case1_convergence(dev):
         opt.zero_grad()
         loss.backward()
         opt.step()
-        if float(loss) < 0.01:
+        if float(loss.detach()) < 0.01:
             assert abs(i - 221) <= 10, i
             return
     raise AssertionError("did not converge")

@@ -125,6 +125,9 @@ def kernel_bytes(w, args, measured=None):
     # transpose in k_vertex_grad's blocks when they are small (DESIGN.md "Kernels"): their bytes then
     # count to the carrying kernel
     if measured is not None:
+        if "k_shade" not in measured:
+            # shading fused into the forward (k_raster_fwd<256, true>): no fim read back
+            k["k_raster_fwd"] += k.pop("k_shade") - fim
         if "k_tex_pack" not in measured:
             k["k_face_setup"] += k.pop("k_tex_pack")
         if "k_tex_out" not in measured:
@@ -226,6 +229,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         images = step(w)
+    # host time to enqueue the steps (Python, autograd, ctypes, launches): below the GPU time, the
+    # run is GPU-bound
+    host_elapsed = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -292,13 +298,17 @@ def main():
                                   "rgb+sil+depth" if args.mode == "rgbsd" else "silhouettes"),
                    "global_batch": world * args.batch, "image_size": args.image_size, "faces": w["F"],
                    "channels": w["C"], "parallelism": "batch-sharded dp%d" % world},
+        "host_ms_per_step": round(host_elapsed / args.steps * 1e3, 4),
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5),
                      "copy_ceiling_gbs": round(ceiling, 1),
                      # the kernel's VALU issue share (PMC pass, tools/pmc_traffic.sh): with the HBM
                      # share this shows the kernel is bound by neither -- latency
-                     "valu_busy": None if valu_busy is None else round(valu_busy, 3)},
+                     "valu_busy": None if valu_busy is None else round(valu_busy, 3),
+                     # what actually limits the kernel: its HBM share and its
+                     # VALU share are both well below 1, i.e. dependent-load latency and issue
+                     "limiter": "latency"},
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "step_roofline_frac": round(total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
     }

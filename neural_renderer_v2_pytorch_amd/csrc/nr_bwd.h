@@ -49,6 +49,9 @@ static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 #ifndef NR_BWD_SKIP_ZERO
 #define NR_BWD_SKIP_ZERO 0  // 1: any all-zero pixel skips the gather (costs the headline ~0.5 %); 0: silhouettes-only renders only
 #endif
+#ifndef NR_BWD_PRELOAD
+#define NR_BWD_PRELOAD 0  // 1: step 1 loads both pixels' face records before either pixel's arithmetic
+#endif
 #ifndef NR_HALO_EARLY
 #define NR_HALO_EARLY 1
 #endif
@@ -69,18 +72,27 @@ struct BwdArgs {
 
 // upstream gradient of internal pixel (x, y): the flip / 2x2-mean backward is an index map and /4.
 // gi: this item's [C, s, s] upstream gradient (32-bit offsets inside it)
+// The MAXC loads are unconditional (channel min(c, C - 1), in bounds) and issued together: a load
+// under the runtime `c < C` branch had its wait inside the branch, which serialised the channels'
+// HBM round trips.  x / 4 == x * 0.25 exactly (power-of-two scale).
+__device__ __forceinline__ void upstream_load(const BwdArgs& a, const float* __restrict__ gi, int C, int y, int x, int S,
+                                              float* raw) {
+    const int s = a.s;
+    const int plane = a.aa ? s * s : S * S;
+    const int o = a.aa ? ((S - 1 - y) >> 1) * s + ((S - 1 - x) >> 1) : (S - 1 - y) * S + (S - 1 - x);
+#pragma unroll
+    for (int c = 0; c < MAXC; c++) raw[c] = gi[min(c, C - 1) * plane + o];
+}
+__device__ __forceinline__ void upstream_scale(const BwdArgs& a, int C, const float* raw, float* G) {
+    const float scale = a.aa ? 0.25f : 1.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; c++) G[c] = c < C ? raw[c] * scale : 0.f;
+}
 __device__ __forceinline__ void upstream_grad(const BwdArgs& a, const float* __restrict__ gi, int C, int y, int x, int S,
                                               float* G) {
-    if (a.aa) {
-        const int s = a.s;
-        const int o = ((S - 1 - y) >> 1) * s + ((S - 1 - x) >> 1);
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) G[c] = c < C ? gi[c * s * s + o] / 4.f : 0.f;
-    } else {
-        const int o = (S - 1 - y) * S + (S - 1 - x);
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) G[c] = c < C ? gi[c * S * S + o] : 0.f;
-    }
+    float raw[MAXC];
+    upstream_load(a, gi, C, y, x, S, raw);
+    upstream_scale(a, C, raw, G);
 }
 
 __device__ __forceinline__ float upstream_one(const BwdArgs& a, const float* __restrict__ gi, int y, int x, int S, int c) {
@@ -221,12 +233,21 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     // ---- 1. image + upstream gradient (LDS), and the stencil-independent gradient terms ---------
     BwdPix P[NPX];
     float I2[NPX][MAXC], G2[NPX][MAXC];
+    // every pixel's face id and upstream gradient loads first, unconditional (clamped in-bounds
+    // coordinates) so they are all in flight together; the image-border mask is applied after
+    int fiv[NPX];
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        const int cy = min(ty0 + ly0 + 4 * k, S - 1), cx = min(px, S - 1);
+        fiv[k] = fimb[cy * S + cx];
+        upstream_load(a, gimb, C, cy, cx, S, G2[k]);
+    }
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
         const int py = ty0 + ly0 + 4 * k;
         const bool inside = px < S && py < S;
         BwdPix& q = P[k];
-        q.fi = inside ? fimb[py * S + px] : -1;
+        q.fi = inside ? fiv[k] : -1;
         q.pos = -1;
         q.wx = q.wy = INT_MIN;
         q.w[0] = q.w[1] = q.w[2] = 0.f;
@@ -234,9 +255,13 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         q.grgb[0] = q.grgb[1] = q.grgb[2] = 0.f;
         q.ay = q.by = q.ax = q.bx = 0.f;
         q.gn[0] = q.gn[1] = q.gn[2] = 0.f;
+        float graw[MAXC];
 #pragma unroll
-        for (int c = 0; c < MAXC; c++) I2[k][c] = G2[k][c] = 0.f;
-        if (inside) upstream_grad(a, gimb, C, py, px, S, G2[k]);
+        for (int c = 0; c < MAXC; c++) {
+            graw[c] = G2[k][c];
+            I2[k][c] = 0.f;
+        }
+        upstream_scale(a, inside ? C : 0, graw, G2[k]);
         if (BG && rgb && inside) {
             // background pixels: rgb = 0 * 0 + 1 * bg (chainer rasterize.py:576); grad of bg = (1 - fg) G
             const float fg = q.fi >= 0 ? 1.f : 0.f;
@@ -253,6 +278,14 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
         }
     }
+#if NR_BWD_PRELOAD
+    // both pixels' face records in flight together (background pixels load face 0's, unused)
+    Face fpre[NPX];
+    if (!wlate && a.F > 0) {
+#pragma unroll
+        for (int k = 0; k < NPX; k++) fpre[k] = load_face_rec(frb + max(P[k].fi, 0) * FACE_REC);
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
         const int py = ty0 + ly0 + 4 * k;
@@ -264,7 +297,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             I2[k][0] = 1.f;
             continue;
         }
+#if NR_BWD_PRELOAD
+        Face f = fpre[k];
+#else
         Face f = load_face_rec(frb + q.fi * FACE_REC);
+#endif
 #ifndef NR_BWD_FASTDIV
         f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
 #endif

@@ -319,15 +319,23 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
 #ifndef NR_FWD_WPE
 #define NR_FWD_WPE 8
 #endif
+#ifndef NR_FWDS_WPE
+#define NR_FWDS_WPE 7  // the fused shading epilogue's live values need more than 64 VGPRs
+#endif
 #ifndef NR_FWD_FORCE_NT
 #define NR_FWD_FORCE_NT 0  // timing builds: 256 / 512 / 1024 threads for every launch
 #endif
-template <int NTF>
-__global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
+// SHADE (NTF == 256, anti-aliasing, no lights / backgrounds): the block also shades its bin's 16x16
+// output pixels (k_shade's work, shade_quad) from the face ids it has just found, so the face-index
+// map is not read back and k_shade has no launch of its own.
+template <int NTF, bool SHADE>
+__global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_FWDS_WPE : NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
-                                                  int32_t* __restrict__ fim) {
+                                                  int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
+                                                  float* __restrict__ halo) {
     using C = FwdCfg<NTF>;
+    static_assert(!SHADE || (NTF == 256 && COARSE == 32), "fused shading: one output pixel per thread");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
     __shared__ int s_scan[C::NW];
@@ -416,6 +424,30 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(NR_FWD_WPE,
         C::block_of(wid, k, ox, oy);
         const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
         if (px < S && py < S) fimb[py * S + px] = best[k];
+    }
+    if (SHADE) {
+        // the bin's 32x32 face ids go through LDS (the staging area is free once every wave has
+        // walked); thread t then shades the output pixel whose internal quad is (2 (t >> 4), 2 (t & 15))
+        Shade sh = sh_in;
+        sh.nl = 0;
+        sh.bg = nullptr;
+        int* s_fim = reinterpret_cast<int*>(s_raw);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NSUB; k++) {
+            int ox, oy;
+            C::block_of(wid, k, ox, oy);
+            s_fim[(oy + (lane >> 3)) * COARSE + ox + (lane & 7)] = best[k];
+        }
+        __syncthreads();
+        const int m = t >> 4, n = t & 15;
+        const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
+        if (iy + 1 < S && ix + 1 < S) {
+            const int2 q0 = *reinterpret_cast<const int2*>(s_fim + (2 * m) * COARSE + 2 * n);      // d, b
+            const int2 q1 = *reinterpret_cast<const int2*>(s_fim + (2 * m + 1) * COARSE + 2 * n);  // c, a
+            const int fis[4] = {q1.y, q0.y, q1.x, q0.x};
+            shade_quad(sh, face_records + (long long)b * F * FACE_REC, b, S, iy, ix, fis, images, halo);
+        }
     }
 }
 

@@ -39,11 +39,15 @@
 
 #include "nr_raster.h"
 
+#ifndef NR_FUSE_SHADE
+#define NR_FUSE_SHADE 1  // 0: k_shade always has its own launch (timing builds)
+#endif
+
 #pragma clang fp contract(off)
 
 #include "nr_common.h"
-#include "nr_fwd.h"
 #include "nr_shade.h"
+#include "nr_fwd.h"
 #include "nr_bwd.h"
 #include "nr_camera.h"
 #include "nr_host.h"
@@ -121,31 +125,37 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             if (e) return e;
         }
     }
+    // k_shade's work fused into the forward's 256-thread variant (anti-aliasing, no lights or
+    // backgrounds): the face-index map is not read back, and there is one launch fewer
+    const long long blocks = (long long)g.nbins * B;
+    const double faces_per_bin = (double)F / g.nbins;
+    const int ntf = NR_FWD_FORCE_NT ? NR_FWD_FORCE_NT : ((blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024);
+    const Shade sh = ra ? make_shade(ra) : Shade{};
+    const bool fuse = NR_FUSE_SHADE && ra && ntf == 256 && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
     {
         ProfScope _p(P_RASTER, st);
         // block size (k_raster_fwd notes): 256 threads when the grid alone fills the chip many times
         // over and the bins are shallow; 1024 when it does not, or when the bins are deep (F per bin
         // at the 32x32 bin granularity as the depth proxy)
-        const long long blocks = (long long)g.nbins * B;
-        const double faces_per_bin = (double)F / g.nbins;
-        const int ntf = NR_FWD_FORCE_NT ? NR_FWD_FORCE_NT : ((blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024);
         const int rs = vertices ? FACE_REC : 9;
-        if (ntf == 256)
-            hipLaunchKernelGGL(k_raster_fwd<256>, dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask, F, g,
-                               near, far, delta, fim);
+        if (fuse)
+            hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
+                               F, g, near, far, delta, fim, sh, images, ra->halo);
+        else if (ntf == 256)
+            hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr);
         else if (ntf == 512)
-            hipLaunchKernelGGL(k_raster_fwd<512>, dim3(g.nbins, B), dim3(512), 0, st, face_records, rs, bbox, mask, F, g,
-                               near, far, delta, fim);
+            hipLaunchKernelGGL((k_raster_fwd<512, false>), dim3(g.nbins, B), dim3(512), 0, st, face_records, rs, bbox, mask,
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr);
         else
-            hipLaunchKernelGGL(k_raster_fwd<1024>, dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox, mask, F, g,
-                               near, far, delta, fim);
+            hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
+                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr);
     }
     int e = check_launch("k_raster_fwd");
-    if (e || !ra) return e;
+    if (e || !ra || fuse) return e;
     const int s = ra->anti_aliasing ? S / 2 : S;
     {
         ProfScope _p(P_SHADE, st);
-        const Shade sh = make_shade(ra);
         if (NR_SHADE_PX == 1 || (NR_SHADE_PX == 2 && ((long long)s * s + 255) / 256 * B < 4096)) {
             const dim3 grid((unsigned)(((long long)s * s + (ra->anti_aliasing ? 63 : 255)) / (ra->anti_aliasing ? 64 : 256)), B);
             switch ((sh.nl ? 1 : 0) | (sh.bg ? 2 : 0)) {

@@ -54,6 +54,55 @@ __device__ __forceinline__ void halo_store(float* __restrict__ halo, int b, int 
 }
 
 // ------------------------------------------------------------------------------------------------
+// One anti-aliased output pixel: the 2x2 average of the flipped image (rasterize.py:321-328).  The
+// internal quad has top-left (iy, ix) and face ids fis = {a, b, c, d} with a = (iy+1, ix+1),
+// b = (iy, ix+1), c = (iy+1, ix), d = (iy, ix); output (oi, oj) = ((S-2-iy)/2, (S-2-ix)/2).  Writes
+// the C channels and the quad's backward-tile-border pixels to the halo cache.  Used by k_shade and by
+// the forward's fused shading epilogue (k_raster_fwd<256, true>).
+__device__ __forceinline__ void shade_quad(const Shade& sh, const float* __restrict__ frb, int b, int S, int iy, int ix,
+                                           const int fis[4], float* __restrict__ images, float* __restrict__ halo) {
+    const int s = S / 2;
+    const int o = ((S - 2 - iy) >> 1) * s + ((S - 2 - ix) >> 1);
+    float* ob = images + (long long)b * sh.C * s * s + o;
+    const int ys[4] = {iy + 1, iy, iy + 1, iy}, xs[4] = {ix + 1, ix + 1, ix, ix};
+    float v[4][MAXC];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        Face f = empty_face();
+        if (fis[q] >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fis[q] * FACE_REC);
+        shade_pixel(sh, b, fis[q], f, xs[q], ys[q], S, v[q]);
+    }
+#pragma unroll
+    for (int c = 0; c < MAXC; c++)
+        if (c < sh.C) ob[c * s * s] = (((v[0][c] + v[1][c]) + v[2][c]) + v[3][c]) / 4.f;
+    if (halo) {
+        // this thread's 2x2 internal pixels on the backward's tile borders: rows iy (top border) /
+        // iy + 1 (bottom border) as float2 pairs, columns ix (left) / ix + 1 (right)
+        float* hb = halo + b * halo_item_floats(S, sh.C);
+        const int C = sh.C;
+        const int ry = iy & (HALO_TH - 1), rx = ix & (HALO_TW - 1);
+        if (ry == 0 || ry == HALO_TH - 2) {
+            const int top = ry == 0, y = top ? iy : iy + 1;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++)
+                if (c < C)
+                    *reinterpret_cast<float2*>(hb + halo_row_offset(C, S, ix, y, c)) =
+                        top ? make_float2(v[3][c], v[1][c]) : make_float2(v[2][c], v[0][c]);
+        }
+        if (rx == 0 || rx == HALO_TW - 2) {
+            const int left = rx == 0, x = left ? ix : ix + 1;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                if (c < C) {
+                    hb[halo_col_offset(C, S, x, iy, c)] = left ? v[3][c] : v[1][c];
+                    hb[halo_col_offset(C, S, x, iy + 1, c)] = left ? v[2][c] : v[0][c];
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_shade: the image channels from the face-index map, one thread per OUTPUT pixel (rasterize.py:
 // 237-328): weights (compute_weight_map), texture sample, silhouette and depth for the 1 or 2x2
 // internal pixels it covers, merged in rgb/sil/depth order, flipped, and 2x2-averaged with the
@@ -99,42 +148,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
     const int2 f0 = *reinterpret_cast<const int2*>(fb + iy * S + ix);        // d, b
     const int2 f1 = *reinterpret_cast<const int2*>(fb + (iy + 1) * S + ix);  // c, a
     const int fis[4] = {f1.y, f0.y, f1.x, f0.x};
-    const int ys[4] = {iy + 1, iy, iy + 1, iy}, xs[4] = {ix + 1, ix + 1, ix, ix};
-    float v[4][MAXC];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        Face f = empty_face();
-        if (fis[q] >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fis[q] * FACE_REC);
-        shade_pixel(sh, b, fis[q], f, xs[q], ys[q], S, v[q]);
-    }
-#pragma unroll
-    for (int c = 0; c < MAXC; c++)
-        if (c < sh.C) ob[c * s * s] = (((v[0][c] + v[1][c]) + v[2][c]) + v[3][c]) / 4.f;
-    if (halo) {
-        // this thread's 2x2 internal pixels on the backward's tile borders: rows iy (top border) /
-        // iy + 1 (bottom border) as float2 pairs, columns ix (left) / ix + 1 (right)
-        float* hb = halo + b * halo_item_floats(S, sh.C);
-        const int C = sh.C;
-        const int ry = iy & (HALO_TH - 1), rx = ix & (HALO_TW - 1);
-        if (ry == 0 || ry == HALO_TH - 2) {
-            const int top = ry == 0, y = top ? iy : iy + 1;
-#pragma unroll
-            for (int c = 0; c < MAXC; c++)
-                if (c < C)
-                    *reinterpret_cast<float2*>(hb + halo_row_offset(C, S, ix, y, c)) =
-                        top ? make_float2(v[3][c], v[1][c]) : make_float2(v[2][c], v[0][c]);
-        }
-        if (rx == 0 || rx == HALO_TW - 2) {
-            const int left = rx == 0, x = left ? ix : ix + 1;
-#pragma unroll
-            for (int c = 0; c < MAXC; c++) {
-                if (c < C) {
-                    hb[halo_col_offset(C, S, x, iy, c)] = left ? v[3][c] : v[1][c];
-                    hb[halo_col_offset(C, S, x, iy + 1, c)] = left ? v[2][c] : v[0][c];
-                }
-            }
-        }
-    }
+    shade_quad(sh, frb, b, S, iy, ix, fis, images, halo);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -389,6 +389,42 @@ def test_headline_sampled_items_vs_oracle(oracle_mod, dev):
         close_grads(pv.grad[i:i + 1], pc.grad, "item %d grad vertices" % i)
 
 
+@pytest.mark.parametrize("mode", ["sil", "depth", "rgba", "rgbsd"])
+def test_fused_forward_shading_matches_separate_shade(dev, mode):
+    """A 32-item batch at 256^2 AA takes the forward with shading fused into the face-index kernel
+    (k_raster_fwd<256, true>: >= 8192 bins, shallow bins); a single item takes the 1024-thread
+    face-index kernel plus k_shade_px.  Same images bit for bit, and the same per-item vertex
+    gradients within the gradient tolerance (the halo cache is written by the fused epilogue in
+    the batch and by k_shade_px alone)."""
+    B = 32
+    proj, f = _ico_batch(4, B, dev)
+    ft_ = torch.as_tensor(f, device=dev)
+    hp = nr.RasterizeHyperparam()
+    hp.draw_rgb = mode in ("rgba", "rgbsd")
+    hp.draw_silhouettes = mode in ("sil", "rgba", "rgbsd")
+    hp.draw_depth = mode in ("depth", "rgbsd")
+    params = nr.RasterizeParam()
+    params1 = nr.RasterizeParam()
+    if hp.draw_rgb:
+        vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+        tex = torch.rand(tex.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+        vt = torch.as_tensor(vt, device=dev)
+        params = nr.RasterizeParam(vertices_textures=vt[None].expand(B, -1, -1), faces_textures=torch.as_tensor(ft, device=dev),
+                                   textures=tex[None].expand(B, -1, -1, -1))
+        params1 = nr.RasterizeParam(vertices_textures=vt[None], faces_textures=torch.as_tensor(ft, device=dev),
+                                    textures=tex[None])
+    pv = proj.to(dev).requires_grad_(True)
+    img = nrr.rasterize_core(pv, ft_, params, hp)
+    g = torch.randn(img.shape, generator=torch.Generator().manual_seed(13)).to(dev)
+    img.backward(g)
+    for i in (0, 17, 31):
+        p1 = proj[i:i + 1].to(dev).requires_grad_(True)
+        img1 = nrr.rasterize_core(p1, ft_, params1, hp)
+        assert torch.equal(img1[0], img[i].detach()), "item %d images" % i
+        img1.backward(g[i:i + 1])
+        close_grads(pv.grad[i:i + 1], p1.grad, "item %d grad vertices" % i)
+
+
 def test_empty_and_degenerate(dev):
     hp = nr.RasterizeHyperparam(image_size=16)
     v = torch.zeros((0, 3, 3), device=dev)

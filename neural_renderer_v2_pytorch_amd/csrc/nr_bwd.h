@@ -27,6 +27,7 @@ constexpr int BH = 16;                        // block height
 constexpr int HW_ = TW + 2, HH_ = BH + 2, HN = HW_ * HH_;
 constexpr int NHALO = 2 * HW_ + 2 * BH;       // 100 halo pixels
 constexpr int TWIN = 4;                       // texel window edge per face
+
 // staged record: ay by ax bx | pos G_rgb[3] | gF[9] | pad (20 floats); with lights also dL/dnormal[3]
 // and the weights w[3] at 17..22 (24 floats)
 template <bool LIT> constexpr int srec() { return LIT ? 24 : 20; }
@@ -48,9 +49,6 @@ static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 #endif
 #ifndef NR_BWD_SKIP_ZERO
 #define NR_BWD_SKIP_ZERO 0  // 1: any all-zero pixel skips the gather (costs the headline ~0.5 %); 0: silhouettes-only renders only
-#endif
-#ifndef NR_BWD_PRELOAD
-#define NR_BWD_PRELOAD 0  // 1: step 1 loads both pixels' face records before either pixel's arithmetic
 #endif
 #ifndef NR_HALO_EARLY
 #define NR_HALO_EARLY 1
@@ -79,7 +77,9 @@ __device__ __forceinline__ void upstream_load(const BwdArgs& a, const float* __r
                                               float* raw) {
     const int s = a.s;
     const int plane = a.aa ? s * s : S * S;
-    const int o = a.aa ? ((S - 1 - y) >> 1) * s + ((S - 1 - x) >> 1) : (S - 1 - y) * S + (S - 1 - x);
+    // 24-bit multiplies (sizes < 2^24): a 64-bit v_mad_u64_u32 here reads an undefined high half
+    // that the compiler's wait insertion treats as a use of an in-flight load's destination
+    const int o = a.aa ? (int)__umul24((S - 1 - y) >> 1, s) + ((S - 1 - x) >> 1) : (int)__umul24(S - 1 - y, S) + (S - 1 - x);
 #pragma unroll
     for (int c = 0; c < MAXC; c++) raw[c] = gi[min(c, C - 1) * plane + o];
 }
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
         const int cy = min(ty0 + ly0 + 4 * k, S - 1), cx = min(px, S - 1);
-        fiv[k] = fimb[cy * S + cx];
+        fiv[k] = fimb[(int)__umul24(cy, S) + cx];
         upstream_load(a, gimb, C, cy, cx, S, G2[k]);
     }
 #pragma unroll
@@ -278,14 +278,6 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
         }
     }
-#if NR_BWD_PRELOAD
-    // both pixels' face records in flight together (background pixels load face 0's, unused)
-    Face fpre[NPX];
-    if (!wlate && a.F > 0) {
-#pragma unroll
-        for (int k = 0; k < NPX; k++) fpre[k] = load_face_rec(frb + max(P[k].fi, 0) * FACE_REC);
-    }
-#endif
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
         const int py = ty0 + ly0 + 4 * k;
@@ -297,11 +289,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             I2[k][0] = 1.f;
             continue;
         }
-#if NR_BWD_PRELOAD
-        Face f = fpre[k];
-#else
         Face f = load_face_rec(frb + q.fi * FACE_REC);
-#endif
+        // the texture record with the face record: one round trip for both (unconditional, so that
+        // no branch join needs its value: without rgb it reads the face record's first 32 bytes)
+        const FaceUV fuv = load_face_uv(rgb ? fuvb + q.fi * 8 : frb + q.fi * FACE_REC);
+        __builtin_amdgcn_sched_barrier(0);  // keeps the scheduler from sinking the uv load to its use
 #ifndef NR_BWD_FASTDIV
         f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
 #endif
@@ -315,7 +307,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
         if (rgb && !(NR_ABLATE & 128)) {
             TexSample s;
-            const float* fuv = fuvb + q.fi * 8;
+            const float uvs[6] = {fuv.a.x, fuv.a.y, fuv.a.z, fuv.a.w, fuv.b.x, fuv.b.y};
             // lights: rgb = texture * cw, so the texture sees G * cw and cw sees G * texture
             float Gt[3] = {G[0], G[1], G[2]};
             float nrm[3], cw[3];
@@ -415,7 +407,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                 const float rz = frcp(s.zq[j]);
                 float gzj = 0.f;
 #pragma unroll
-                for (int qq = 0; qq < 2; qq++) gzj += (-(gpr[qq] * s.dt)) * (w[j] * fuv[2 * j + qq]) * rz * rz;
+                for (int qq = 0; qq < 2; qq++) gzj += (-(gpr[qq] * s.dt)) * (w[j] * uvs[2 * j + qq]) * rz * rz;
                 gzj += (-g_st) * w[j] * rz * rz;
                 q.gz[j] = gzj;
             }
@@ -484,9 +476,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
         if (!(NR_ABLATE & 16) && h_in) {
             const int hf = fimb[hpy * S + hpx];
-            Face ff = empty_face();
-            if (hf >= 0 && shade_needs_face(sh)) ff = load_face_rec(frb + hf * FACE_REC);
-            shade_pixel(sh, b, hf, ff, hpx, hpy, S, hI);
+            Face ff;
+            FaceUV fu;
+            load_shading_face(sh, frb, b, hf, ff, fu);
+            shade_pixel(sh, b, hf, ff, fu, hpx, hpy, S, hI);
             upstream_grad(a, gimb, C, hpy, hpx, S, hG);
         }
         const int hl = hy * HW_ + hx;
@@ -881,7 +874,7 @@ __global__ __launch_bounds__(256) void k_param_bwd(BwdArgs a, Shade sh, int S, c
         const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + fi * 8;
         TexSample s;
         float gw[4];
-        sample_texture(f, w, false, fuv, sh.tv, bt, sh.eps, s, Gt, gw);
+        sample_texture(f, w, false, load_face_uv(fuv), sh.tv, bt, sh.eps, s, Gt, gw);
         T[0] = s.rgb[0];
         T[1] = s.rgb[1];
         T[2] = s.rgb[2];

@@ -242,14 +242,26 @@ struct TexSample {
     float rgb[3];
 };
 
-// uv: the face's 8-float texture record (u0 v0 u1 v1 u2 v2, flag, -); flag 1 = every u, v in
-// {0} u [2^-16, 2^20].  wfast: face_weights took its exact-division path.
+// The face's 8-float texture record (u0 v0 u1 v1 u2 v2, flag, -); flag 1 = every u, v in
+// {0} u [2^-16, 2^20].  Callers load it together with the face record (both depend only on the face
+// id), so the two are one memory round trip, not two.
+struct FaceUV {
+    float4 a, b;
+};
+__device__ __forceinline__ FaceUV load_face_uv(const float* __restrict__ uv) {
+    FaceUV u;
+    u.a = reinterpret_cast<const float4*>(uv)[0];
+    u.b = reinterpret_cast<const float4*>(uv)[1];
+    return u;
+}
+
+// wfast: face_weights took its exact-division path.
 // G (optional, backward): upstream gradient of the rgb channels; then gw[i] = sum_c G[c] T_i[c] for
 // the 4 bilinear texels, from the texel values loaded here (no second load)
-__device__ __forceinline__ void sample_texture(const Face& f, const float w[3], bool wfast, const float* __restrict__ uv,
+__device__ __forceinline__ void sample_texture(const Face& f, const float w[3], bool wfast, const FaceUV& uvr,
                                                const TexView& tv, int bt, float eps, TexSample& s,
                                                const float* G = nullptr, float* gw = nullptr) {
-    const float4 uva = reinterpret_cast<const float4*>(uv)[0], uvb = reinterpret_cast<const float4*>(uv)[1];
+    const float4 uva = uvr.a, uvb = uvr.b;
     const float uvs[6] = {uva.x, uva.y, uva.z, uva.w, uvb.x, uvb.y};
     const bool fast = wfast && (f.flags & FACE_FAST_ZQ) && __float_as_int(uvb.z) != 0;
     const float z[3] = {f.z0, f.z1, f.z2};
@@ -427,8 +439,25 @@ __device__ __forceinline__ void background(const Shade& sh, int b, int x, int y,
 // All channels of one internal pixel (rasterize.py:295-310 merge order: rgb, sil, depth), written
 // to compile-time slots of out[MAXC] (runtime-indexed register arrays would spill to scratch).
 __device__ __forceinline__ bool shade_needs_face(const Shade& sh) { return (sh.draw & (NR_DRAW_RGB | NR_DRAW_DEPTH)) != 0; }
-__device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, int x, int y, int S,
-                                            float* out) {
+
+// A zero record: the address the shading loads read for pixels that need no face.
+__device__ float k_zero_rec[FACE_REC] = {};  // never written (a global, so the loads stay global_load)
+
+// The face record and (rgb) texture record of pixel face id fi, loaded together and without a branch:
+// a load under a branch has its wait at the branch join, which serialises the pixels' round trips.
+// Pixels that need no face (background, or a render without rgb / depth) read k_zero_rec; shade_pixel
+// ignores their values.
+__device__ __forceinline__ void load_shading_face(const Shade& sh, const float* __restrict__ frb, int b, int fi, Face& f,
+                                                  FaceUV& u) {
+    const bool need = fi >= 0 && shade_needs_face(sh);
+    f = load_face_rec(need ? frb + fi * FACE_REC : k_zero_rec);
+    u = load_face_uv(need && (sh.draw & NR_DRAW_RGB)
+                         ? sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + fi * 8
+                         : k_zero_rec);
+}
+
+__device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, const FaceUV& fuv, int x, int y,
+                                            int S, float* out) {
     const bool R = (sh.draw & NR_DRAW_RGB) != 0, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
     const float xp = pix_center(x, S), yp = pix_center(y, S);
     float r = 0.f, gg = 0.f, bb = 0.f, sil = 0.f, dep = 0.f;
@@ -439,7 +468,6 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
         const bool wfast = face_weights(xp, yp, f, w);
         if (R) {
             TexSample s;
-            const float* fuv = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0) + fi * 8;
             sample_texture(f, w, wfast, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s);
             r = s.rgb[0];
             gg = s.rgb[1];

@@ -68,9 +68,10 @@ __device__ __forceinline__ void shade_quad(const Shade& sh, const float* __restr
     float v[4][MAXC];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        Face f = empty_face();
-        if (fis[q] >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fis[q] * FACE_REC);
-        shade_pixel(sh, b, fis[q], f, xs[q], ys[q], S, v[q]);
+        Face f;
+        FaceUV u;
+        load_shading_face(sh, frb, b, fis[q], f, u);
+        shade_pixel(sh, b, fis[q], f, u, xs[q], ys[q], S, v[q]);
     }
 #pragma unroll
     for (int c = 0; c < MAXC; c++)
@@ -132,10 +133,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
         // permute to [B, C, S, S] and flip both axes (rasterize.py:315-316)
         const int y = S - 1 - oi, x = S - 1 - oj;
         const int fi = fb[y * S + x];
-        Face f = empty_face();
-        if (fi >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fi * FACE_REC);
+        Face f;
+        FaceUV u;
+        load_shading_face(sh, frb, b, fi, f, u);
         float v[MAXC];
-        shade_pixel(sh, b, fi, f, x, y, S, v);
+        shade_pixel(sh, b, fi, f, u, x, y, S, v);
 #pragma unroll
         for (int c = 0; c < MAXC; c++)
             if (c < sh.C) ob[c * s * s] = v[c];
@@ -196,10 +198,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
         x = S - 1 - oj;
     }
     const int fi = fb[y * S + x];
-    Face f = empty_face();
-    if (fi >= 0 && shade_needs_face(sh)) f = load_face_rec(frb + fi * FACE_REC);
+    Face f;
+    FaceUV u;
+    load_shading_face(sh, frb, b, fi, f, u);
     float v[MAXC];
-    shade_pixel(sh, b, fi, f, x, y, S, v);
+    shade_pixel(sh, b, fi, f, u, x, y, S, v);
     const bool live = o < s * s;
     if (halo && live) halo_store(halo, b, sh.C, S, x, y, v);
     float* ob = images + (long long)b * sh.C * s * s + o;

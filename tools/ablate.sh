@@ -15,11 +15,14 @@ for V in $VARIANTS; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math \
     -fvisibility=hidden -Iinclude $DEFS neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip -o $OUT/lib/libnr_$i.so || exit 1
 done
+# REPEAT=n runs the whole variant list n times, interleaved (box-to-box and run-to-run spread is a
+# few per cent); STEPS sets the timed steps per run
+for r in $(seq 1 ${REPEAT:-1}); do
 i=0
 for V in $VARIANTS; do
   i=$((i+1))
-  NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_$i.log 2>&1
-  rc=$?; echo "$V rc=$rc: $(python -c "import json,sys; d=json.loads(open('$OUT/bench_$i.log').read().strip().splitlines()[-1]); print(d['kernels_ms'], d['ms_per_step'])")"
+  NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline > $OUT/bench_${i}_$r.log 2>&1
+  rc=$?; echo "$V rc=$rc: $(python -c "import json,sys; d=json.loads(open('$OUT/bench_${i}_$r.log').read().strip().splitlines()[-1]); print(d['kernels_ms'], d['ms_per_step'])")"
   if [ $rc -ne 0 ]; then exit $rc; fi
   if [ -n "$CONFIGS" ]; then
     NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python tools/bench_configs.py --loop-steps 20 --only $CONFIGS > $OUT/configs_$i.log 2>&1
@@ -29,5 +32,6 @@ for l in open('$OUT/configs_$i.log'):
     if l.startswith('{'): d = json.loads(l); print('   ', d['config'][:5], d['ms_per_step'], d['kernels_ms'])"
     if [ $rc -ne 0 ]; then exit $rc; fi
   fi
+done
 done
 rm -rf $OUT/lib

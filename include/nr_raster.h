@@ -117,7 +117,9 @@ typedef struct NrRasterArgs {
      * vertex_faces[vertex_offsets[v] .. vertex_offsets[v+1]) lists 3 f + k for every faces[f, k] == v. */
     const int32_t* vertex_offsets; /* [V + 1] */
     const int32_t* vertex_faces;   /* [3 F] */
-    /* optional halo cache, nr_halo_bytes() bytes: when set, the forward stores the internal-image
+    /* optional halo cache, nr_halo_bytes() bytes (the tile-border image values, then one byte per
+     * 32x32 bin and item: "the bin has a foreground pixel", which lets the backward skip background
+     * tiles): when set, the forward stores the internal-image
      * values of the backward's tile borders there and the backward reads them instead of shading
      * its tile halos again; NULL = backward re-shades (same results). */
     float* halo;

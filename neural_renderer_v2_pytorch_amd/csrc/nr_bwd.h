@@ -50,8 +50,28 @@ static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 #ifndef NR_BWD_SKIP_ZERO
 #define NR_BWD_SKIP_ZERO 0  // 1: any all-zero pixel skips the gather (costs the headline ~0.5 %); 0: silhouettes-only renders only
 #endif
+#ifndef NR_BWD_SKIP_BG
+#define NR_BWD_SKIP_BG 1  // 0: background tiles run the whole kernel (timing builds)
+#endif
 #ifndef NR_HALO_EARLY
 #define NR_HALO_EARLY 1
+#endif
+
+// per-wave phase timestamps (timing builds only, tools/bwd_timing.py): lane 0 of every wave of the
+// 2-pixel variant records the shader clock at 8 points of its life
+#ifdef NR_BWD_TIMING
+constexpr long long NR_TIMING_MAX = 1 << 22;
+__device__ unsigned long long g_bwd_t[NR_TIMING_MAX];
+#define NR_TSTAMP(k)                                                                                       \
+    do {                                                                                                   \
+        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 8 + (k); \
+        const unsigned long long t_ = clock64();                                                           \
+        if ((threadIdx.x & 63) == 0 && i_ < NR_TIMING_MAX) g_bwd_t[i_] = t_;                                 \
+    } while (0)
+#else
+#define NR_TSTAMP(k) \
+    do {             \
+    } while (0)
 #endif
 
 struct BwdArgs {
@@ -61,6 +81,7 @@ struct BwdArgs {
     float* __restrict__ grad_faces;   // [B, F, 9]
     float* __restrict__ grad_tex4;    // [Bt, HWp, 4] or null
     const float* __restrict__ halo;   // halo cache written by the forward, or null (re-shade the halo)
+    const uint8_t* __restrict__ binfg; // per (item, 32x32 bin) foreground flags after the halo values, or null
     float* __restrict__ grad_normals; // [B, F, 9] per-face corner vertex-normal gradients (lights)
     float* __restrict__ grad_bg;      // [B, 3, S, S] or null
     int F, aa, s, HWp;
@@ -178,6 +199,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     xcd_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(blockIdx.x, b, (S + TW - 1) / TW, (S + BH - 1) / BH, tile_x, tile_y);
     const int tx0 = tile_x * TW;
     const int ty0 = tile_y * BH;
+    // a tile with no foreground pixel contributes nothing (every gradient term is per foreground
+    // pixel; the halo only feeds foreground pixels' stencils): with the forward's bin flags it ends
+    // here.  Backgrounds (BG) get gradient from background pixels, so that instantiation never skips.
+    if (NR_BWD_SKIP_BG && !BG && a.binfg && a.binfg[(long long)b * g.nbins + (ty0 / COARSE) * g.nbx + tx0 / COARSE] == 0) return;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     const int bt = sh.tv.sb ? b : 0;
@@ -226,6 +251,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
         }
     };
+    NR_TSTAMP(0);
 #if NR_HALO_EARLY
     halo_prefetch();  // in flight during step 1
 #endif
@@ -491,7 +517,9 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
         }
     }
+    NR_TSTAMP(1);
     __syncthreads();
+    NR_TSTAMP(2);
 
     // ---- 2. Differentiation.backward stencil -> coordinate-map gradient ------------------------
     float gF[NPX][9];
@@ -544,7 +572,9 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             for (int j = 0; j < 9; j++) asm volatile("" ::"v"(gF[k][j]));
         return;
     }
+    NR_TSTAMP(3);
     __syncthreads();  // the staged records reuse the image / gradient LDS
+    NR_TSTAMP(4);
 
     // ---- 3. stage this lane's two pixel records; group the wave's records by face --------------
     float* rec = s_raw + wid * (64 * NPX * REC);
@@ -591,12 +621,19 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     }
     const bool act0 = P[0].fi >= 0 && nz[0], act1 = fi1 >= 0 && nz[NPX - 1];
     unsigned long long p0 = __ballot(act0), p1 = __ballot(act1);
+    NR_TSTAMP(5);
     // texel lanes: consecutive faces with the same texel window (e.g. every face of a flat-colour
     // material samples one 2x2 atlas patch, load_obj.py:84-94) accumulate into `pend` and flush once
     // per run, so such hot texels take one atomic per run instead of one per face
     float pend = 0.f;
     int pwx = INT_MIN, pwy = 0;
+#ifdef NR_BWD_TIMING
+    int nfaces_dbg = 0;
+#endif
     while (p0 | p1) {
+#ifdef NR_BWD_TIMING
+        nfaces_dbg++;
+#endif
         // leader: lowest pending pixel; both candidates read without branches, selected on the scalar unit
         const bool from0 = p0 != 0ull;
         const int l0 = from0 ? __builtin_ctzll(p0) : 0, l1 = p1 ? __builtin_ctzll(p1) : 0;
@@ -675,6 +712,13 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
             unsafeAtomicAdd(g4b + (y * sh.tv.W + x) * 4 + chunk, pend);
     }
+    NR_TSTAMP(6);
+#ifdef NR_BWD_TIMING
+    {
+        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 8 + 7;
+        if (lane == 0 && i_ < NR_TIMING_MAX) g_bwd_t[i_] = (unsigned long long)nfaces_dbg;
+    }
+#endif
 }
 
 // pixels per lane, per launch: 2 (256 threads) when the grid fills the chip many times over; 1 (512

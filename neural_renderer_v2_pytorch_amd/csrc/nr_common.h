@@ -311,7 +311,14 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
     if (tv.t4) {
         const float4* t4b = tv.t4 + (long long)bt * tv.HWp;
 #pragma unroll
-        for (int i = 0; i < 4; i++) q4[i] = t4b[s.idx[i]];
+        for (int i = 0; i < 4; i++) {
+#if defined(NR_ABLATE_TEX) && (NR_ABLATE_TEX & 1)
+            q4[i] = make_float4(s.wt[i], s.x, s.y, 0.f);  // timing build: no texel loads
+            (void)t4b;
+#else
+            q4[i] = t4b[s.idx[i]];
+#endif
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < 4; i++) off[i] = s.idx[i] * tv.sp;

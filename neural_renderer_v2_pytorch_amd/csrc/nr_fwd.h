@@ -333,7 +333,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
                                                   int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
-                                                  float* __restrict__ halo) {
+                                                  float* __restrict__ halo, uint8_t* __restrict__ binfg) {
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || (NTF == 256 && COARSE == 32), "fused shading: one output pixel per thread");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
@@ -424,6 +424,13 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         C::block_of(wid, k, ox, oy);
         const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
         if (px < S && py < S) fimb[py * S + px] = best[k];
+    }
+    if (binfg) {  // does the bin hold a foreground pixel (the backward skips its tiles when not)
+        bool fg = false;
+#pragma unroll
+        for (int k = 0; k < NSUB; k++) fg = fg || best[k] >= 0;
+        fg = __syncthreads_or(fg) != 0;
+        if (t == 0) binfg[(long long)b * g.nbins + bin] = fg ? 1 : 0;
     }
     if (SHADE) {
         // the bin's 32x32 face ids go through LDS (the staging area is free once every wave has

@@ -132,6 +132,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     const int ntf = NR_FWD_FORCE_NT ? NR_FWD_FORCE_NT : ((blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024);
     const Shade sh = ra ? make_shade(ra) : Shade{};
     const bool fuse = NR_FUSE_SHADE && ra && ntf == 256 && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
+    // per-bin foreground flags after the halo values (the backward skips background tiles)
+    uint8_t* binfg = (ra && ra->halo) ? (uint8_t*)ra->halo + halo_flags_offset_bytes(B, S, sh.C) : nullptr;
     {
         ProfScope _p(P_RASTER, st);
         // block size (k_raster_fwd notes): 256 threads when the grid alone fills the chip many times
@@ -140,16 +142,16 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         const int rs = vertices ? FACE_REC : 9;
         if (fuse)
             hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, images, ra->halo);
+                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
         else if (ntf == 256)
             hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, nullptr, nullptr);
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg);
         else if (ntf == 512)
             hipLaunchKernelGGL((k_raster_fwd<512, false>), dim3(g.nbins, B), dim3(512), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, nullptr, nullptr);
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg);
         else
             hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr);
+                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra || fuse) return e;
@@ -256,7 +258,9 @@ size_t nr_texture_packed_bytes(int texture_items, int tex_height, int tex_width)
 size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw_flags) {
     const int S = anti_aliasing ? 2 * image_size : image_size;
     if (batch_size <= 0 || image_size <= 0) return 0;
-    return (size_t)batch_size * halo_item_floats(S, nr_num_channels(draw_flags)) * sizeof(float);
+    const Geom g = make_geom(0, S);
+    return (size_t)halo_flags_offset_bytes(batch_size, S, nr_num_channels(draw_flags)) +
+           (((size_t)batch_size * g.nbins + 3) & ~size_t(3));
 }
 
 size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num_vertices, int texture_items,
@@ -313,6 +317,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.grad_faces = gF;
     ba.grad_tex4 = rgb ? g4 : nullptr;
     ba.halo = a->halo;
+    ba.binfg = a->halo ? (const uint8_t*)a->halo + halo_flags_offset_bytes(a->batch_size, S, nr_num_channels(a->draw_flags))
+                       : nullptr;
     ba.grad_normals = gN;
     ba.grad_bg = (a->draw_flags & NR_DRAW_RGB) && a->backgrounds ? a->grad_backgrounds : nullptr;
     ba.F = a->num_faces;
@@ -493,6 +499,16 @@ int nr_selftest_division(const float* a, const float* b, float* q_fast, float* q
                        q_fast, q_ieee, n);
     return check_launch("k_selftest_div");
 }
+
+#ifdef NR_BWD_TIMING
+// timing builds only: the backward's per-wave phase timestamps (g_bwd_t), n entries to host memory
+__attribute__((visibility("default"))) int nr_debug_bwd_timing(unsigned long long* out, size_t n) {
+    if (n > (size_t)NR_TIMING_MAX) n = NR_TIMING_MAX;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_t), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(NR_ERR_LAUNCH, "hipMemcpyFromSymbol failed");
+    return NR_OK;
+}
+#endif
 
 int nr_profile_enable(int on) {
     if (on && !g_prof) {

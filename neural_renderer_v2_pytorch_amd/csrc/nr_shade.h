@@ -19,6 +19,11 @@ __host__ __device__ __forceinline__ long long halo_item_floats(int S, int C) {
     const long long nty = (S + HALO_TH - 1) / HALO_TH, ntx = (S + HALO_TW - 1) / HALO_TW;
     return nty * 2 * C * (long long)S + nty * C * HALO_TH * ntx * 2;
 }
+// after the B items' halo values: one byte per (item, 32x32 bin), nonzero when the bin has a
+// foreground pixel (written by the forward, read by the backward to skip background tiles)
+__host__ __device__ __forceinline__ long long halo_flags_offset_bytes(int B, int S, int C) {
+    return (long long)B * halo_item_floats(S, C) * 4;
+}
 __device__ __forceinline__ int halo_row_offset(int C, int S, int x, int y, int c) {
     return (((y / HALO_TH) * 2 + ((y & (HALO_TH - 1)) != 0)) * C + c) * S + x;
 }

@@ -1,0 +1,57 @@
+"""Per-wave phase timing of k_raster_bwd on the headline workload (timing build, NR_BWD_TIMING).
+
+usage (GPU box): python tools/bwd_timing.py [extra -D flags...]
+Builds the library with -DNR_BWD_TIMING into /tmp, runs bench.py's headline step through it, reads
+the per-wave shader-clock stamps of the last backward (nr_debug_bwd_timing) and prints the mean and
+percentiles of each phase: step 1 (recompute + staging of I and G), barrier 1, stencil, barrier 2,
+record staging + grouping, per-face gather + atomics, and the whole wave lifetime."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+lib_path = "/tmp/libnr_timing.so"
+subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                       "-ffp-contract=off", "-fno-fast-math", "-fvisibility=hidden", "-DNR_BWD_TIMING", "-I" + ROOT + "/include"]
+                      + sys.argv[1:] + [ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib_path])
+os.environ["NR_LIB_PATH"] = lib_path
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import bench  # noqa: E402
+
+sys.argv = [sys.argv[0]]
+args = bench.parse()
+torch.cuda.set_device(0)
+w = bench.workload(args, 0, torch.device("cuda", 0))
+for _ in range(4):
+    bench.step(w)
+torch.cuda.synchronize()
+from neural_renderer_v2_pytorch_amd import _lib  # noqa: E402
+L = _lib.lib()
+S = 2 * args.image_size
+blocks = (S // 32) * (S // 16) * args.batch
+n = blocks * 4 * 8
+buf = (ctypes.c_ulonglong * n)()
+assert L.nr_debug_bwd_timing(buf, ctypes.c_size_t(n)) == 0
+t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(blocks, 4, 8)
+names = ["step1", "barrier1", "stencil", "barrier2", "stage+group", "gather+atomics"]
+d = np.diff(t[:, :, :7], axis=2)
+life = t[:, :, 6] - t[:, :, 0]
+print("waves %d, kernel span %.0f clocks" % (blocks * 4, t[:, :, 6].max() - t[:, :, 0].min()))
+for i, nm in enumerate(names):
+    x = d[:, :, i].ravel()
+    print("%-16s mean %8.0f  p10 %8.0f  p50 %8.0f  p90 %8.0f  share %.3f" % (
+        nm, x.mean(), *np.percentile(x, [10, 50, 90]), x.mean() / life.mean()))
+print("%-16s mean %8.0f  p10 %8.0f  p50 %8.0f  p90 %8.0f" % ("lifetime", life.mean(), *np.percentile(life, [10, 50, 90])))
+nf = t[:, :, 7].ravel()
+print("faces per wave: mean %.2f p10/p50/p90 %s max %d" % (nf.mean(), np.percentile(nf, [10, 50, 90]), nf.max()))
+for k in (1, 2, 3, 4, 6, 8):
+    sel = (t[:, :, 7] == k)
+    if sel.any():
+        print("  %d faces: %6d waves, gather mean %7.0f p50 %7.0f, lifetime mean %7.0f" % (
+            k, sel.sum(), d[:, :, 5][sel].mean(), np.median(d[:, :, 5][sel]), life[sel].mean()))
+starts = np.sort(t[:, :, 0].min(axis=1) - t[:, :, 0].min())
+print("block start times (clocks) p10/p50/p90: %s" % np.percentile(starts, [10, 50, 90]).round())

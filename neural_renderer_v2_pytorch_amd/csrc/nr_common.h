@@ -567,12 +567,16 @@ __device__ __forceinline__ void xcd_tile(int L, int b, int nx, int ny, int& tx, 
 template <int NW = NT / 64>
 __device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // inclusive wave scan with DPP (VALU lane shifts, no LDS round trips): row_shr 1, 2, 4, 8 within
+    // the 16-lane rows (bound_ctrl: lanes shifted in from outside the row read 0), then row_bcast:15
+    // adds row r's last lane to row r + 1 and row_bcast:31 lane 31 to rows 2 and 3
     int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     if (lane == 63) lds4[wid] = x;
     __syncthreads();
     int base = 0, tot = 0;

@@ -316,11 +316,27 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
     e[7 * FST] = make_float4(rcp_nr(z2), 0.f, 0.f, __int_as_float(ok ? 1 : 0));
 }
 
+// per-wave phase timestamps of the fused forward (timing builds only, tools/fwd_timing.py)
+#ifdef NR_FWD_TIMING
+constexpr long long NR_FTIMING_MAX = 1 << 21;
+__device__ unsigned long long g_fwd_t[NR_FTIMING_MAX];
+#define NR_FTSTAMP(k, v)                                                                                   \
+    do {                                                                                                   \
+        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 8 + (k); \
+        const unsigned long long t_ = (v);                                                                 \
+        if (SHADE && (threadIdx.x & 63) == 0 && i_ < NR_FTIMING_MAX) g_fwd_t[i_] = t_;                       \
+    } while (0)
+#else
+#define NR_FTSTAMP(k, v) \
+    do {                 \
+    } while (0)
+#endif
+
 #ifndef NR_FWD_WPE
 #define NR_FWD_WPE 8
 #endif
 #ifndef NR_FWDS_WPE
-#define NR_FWDS_WPE 7  // the fused shading epilogue's live values need more than 64 VGPRs
+#define NR_FWDS_WPE 8  // 8 waves/SIMD (a few spilled registers in the shading epilogue; 7 waves measured 3 % slower)
 #endif
 #ifndef NR_FWD_FORCE_NT
 #define NR_FWD_FORCE_NT 0  // timing builds: 256 / 512 / 1024 threads for every launch
@@ -374,11 +390,15 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     const float* frb = face_records + (long long)b * F * rs;
     int32_t* __restrict__ fimb = fim + (long long)b * S * S;
 
+    NR_FTSTAMP(0, clock64());
+    int ncand = 0;  // the bin's candidate faces (block-uniform)
     for (int wbase = 0; wbase < g.nwords; wbase += NTF) {
         const int w = wbase + t;
         const uint32_t bits = (w < g.nwords) ? words[w] : 0u;
         int total;
         const int off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
+        ncand += total;
+        NR_FTSTAMP(1, clock64());
         for (int cbase = 0; cbase < total; cbase += CAND) {
             // expand my word's set bits into the ordered candidate list
             int r = off;
@@ -396,6 +416,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
                     stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
                 }
                 __syncthreads();
+                NR_FTSTAMP(2, clock64());
 #pragma unroll
                 for (int k = 0; k < NSUB; k++) {
                     const float xc0 = xcl[k], xc1 = xch[k], yc0 = ycl[k], yc1 = ych[k];
@@ -418,6 +439,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         }
     }
 
+    NR_FTSTAMP(3, clock64());
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
         int ox, oy;
@@ -425,12 +447,17 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
         if (px < S && py < S) fimb[py * S + px] = best[k];
     }
-    if (binfg) {  // does the bin hold a foreground pixel (the backward skips its tiles when not)
-        bool fg = false;
-#pragma unroll
-        for (int k = 0; k < NSUB; k++) fg = fg || best[k] >= 0;
-        fg = __syncthreads_or(fg) != 0;
-        if (t == 0) binfg[(long long)b * g.nbins + bin] = fg ? 1 : 0;
+    // may the bin hold a foreground pixel (the backward skips its tiles when not): a bin without
+    // candidate faces holds none
+    if (binfg && t == 0) binfg[(long long)b * g.nbins + bin] = ncand > 0 ? 1 : 0;
+    if (SHADE && ncand == 0) {
+        // an empty bin: every channel of its output pixels is 0 (sil, depth and rgb of background;
+        // no backgrounds in this variant), as is every halo value
+        Shade sh = sh_in;
+        const int m = t >> 4, n = t & 15;
+        const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
+        if (iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, halo);
+        return;
     }
     if (SHADE) {
         // the bin's 32x32 face ids go through LDS (the staging area is free once every wave has
@@ -447,6 +474,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
             s_fim[(oy + (lane >> 3)) * COARSE + ox + (lane & 7)] = best[k];
         }
         __syncthreads();
+        NR_FTSTAMP(4, clock64());
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
         if (iy + 1 < S && ix + 1 < S) {
@@ -455,6 +483,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
             const int fis[4] = {q1.y, q0.y, q1.x, q0.x};
             shade_quad(sh, face_records + (long long)b * F * FACE_REC, b, S, iy, ix, fis, images, halo);
         }
+        NR_FTSTAMP(5, clock64());
+        NR_FTSTAMP(6, (unsigned long long)ncand);
     }
 }
 

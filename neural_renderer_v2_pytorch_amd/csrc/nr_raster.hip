@@ -500,6 +500,15 @@ int nr_selftest_division(const float* a, const float* b, float* q_fast, float* q
     return check_launch("k_selftest_div");
 }
 
+#ifdef NR_FWD_TIMING
+// timing builds only: the fused forward's per-wave phase timestamps (g_fwd_t)
+__attribute__((visibility("default"))) int nr_debug_fwd_timing(unsigned long long* out, size_t n) {
+    if (n > (size_t)NR_FTIMING_MAX) n = NR_FTIMING_MAX;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_t), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(NR_ERR_LAUNCH, "hipMemcpyFromSymbol failed");
+    return NR_OK;
+}
+#endif
 #ifdef NR_BWD_TIMING
 // timing builds only: the backward's per-wave phase timestamps (g_bwd_t), n entries to host memory
 __attribute__((visibility("default"))) int nr_debug_bwd_timing(unsigned long long* out, size_t n) {

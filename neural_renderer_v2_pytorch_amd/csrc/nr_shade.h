@@ -108,6 +108,38 @@ __device__ __forceinline__ void shade_quad(const Shade& sh, const float* __restr
     }
 }
 
+// shade_quad for a quad of background pixels without backgrounds: every value is 0
+__device__ __forceinline__ void shade_quad_empty(const Shade& sh, int b, int S, int iy, int ix, float* __restrict__ images,
+                                                 float* __restrict__ halo) {
+    const int s = S / 2;
+    const int o = ((S - 2 - iy) >> 1) * s + ((S - 2 - ix) >> 1);
+    float* ob = images + (long long)b * sh.C * s * s + o;
+#pragma unroll
+    for (int c = 0; c < MAXC; c++)
+        if (c < sh.C) ob[c * s * s] = 0.f;
+    if (halo) {
+        float* hb = halo + b * halo_item_floats(S, sh.C);
+        const int C = sh.C;
+        const int ry = iy & (HALO_TH - 1), rx = ix & (HALO_TW - 1);
+        if (ry == 0 || ry == HALO_TH - 2) {
+            const int y = ry == 0 ? iy : iy + 1;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++)
+                if (c < C) *reinterpret_cast<float2*>(hb + halo_row_offset(C, S, ix, y, c)) = make_float2(0.f, 0.f);
+        }
+        if (rx == 0 || rx == HALO_TW - 2) {
+            const int x = rx == 0 ? ix : ix + 1;
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                if (c < C) {
+                    hb[halo_col_offset(C, S, x, iy, c)] = 0.f;
+                    hb[halo_col_offset(C, S, x, iy + 1, c)] = 0.f;
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_shade: the image channels from the face-index map, one thread per OUTPUT pixel (rasterize.py:
 // 237-328): weights (compute_weight_map), texture sample, silhouette and depth for the 1 or 2x2

@@ -236,9 +236,28 @@ template <int NTF> struct FwdCfg {
 
 // the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel; q0, q1 are
 // the record's first two float4 (loaded ahead by the caller); FST = the SoA stride (FCAP)
+// NR_FWD_EAGER: how many of the record's float4 rows the walk loads before the first test (2: the
+// tests load the rest as they go; 6: one LDS round trip for the depth, box and edge tests; 8: all)
+#ifndef NR_FWD_EAGER
+#define NR_FWD_EAGER 6  // measured: 2 -> 6 takes the headline forward 0.268 -> 0.259 ms, the car 1.20 -> 1.14 ms; 8 spills
+#endif
 template <int FST>
-__device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1, float xp, float yp, float near, float far,
+struct FaceRows {
+    float4 r[8];
+    __device__ __forceinline__ void load(const float4* e) {
+#pragma unroll
+        for (int i = 0; i < NR_FWD_EAGER; i++) r[i] = e[i * FST];
+        // an empty asm that takes the rows keeps the compiler from sinking each load into the branch
+        // that first uses it (which costs an LDS round trip per test stage)
+#pragma unroll
+        for (int i = 0; i < NR_FWD_EAGER; i++) asm volatile("" ::"v"(r[i].x), "v"(r[i].y), "v"(r[i].z), "v"(r[i].w));
+    }
+    __device__ __forceinline__ float4 get(const float4* e, int i) const { return i < NR_FWD_EAGER ? r[i] : e[i * FST]; }
+};
+template <int FST>
+__device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& fr, float xp, float yp, float near, float far,
                                           float delta, float& depth_min, int& best) {
+    const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1);
 #if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 1
     best += (int)q0.x;  // timing build: no per-pixel test
     return;
@@ -249,7 +268,7 @@ __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1,
     if (depth_min < q1.z) return;
     // .cu:94-97 (min/max form, exact for non-NaN faces)
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
-    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
+    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4), q5 = fr.get(e, 5);
     const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
     // .cu:107-116
     const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
@@ -261,7 +280,7 @@ __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1,
     best = __float_as_int(q1.w);  // timing build: no division block
     return;
 #endif
-    const float4 q6 = e[6 * FST];
+    const float4 q6 = fr.get(e, 6);
     const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
     // .cu:130-139
     float w0 = (yp * q4.w - xp * q5.x) + q5.w;
@@ -269,7 +288,7 @@ __device__ __forceinline__ void face_test(const float4* e, float4 q0, float4 q1,
     float w2 = (yp * q4.y - xp * q4.z) + q6.y;
     const float ws = w0 + w1 + w2;
     float zp;
-    const float4 q7 = e[7 * FST];
+    const float4 q7 = fr.get(e, 7);
     if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
         // face coordinates and depths within [2^-20, 2^20] (or 0) bound every operand below inside
         // div_nr's exact range (DESIGN.md "Numerics"); 1/z is staged per face
@@ -366,7 +385,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     const int bx0 = bin_x * COARSE;
     const int by0 = bin_y * COARSE;
     const int t = threadIdx.x;
-    const int lane = t & 63, wid = t >> 6;
+    const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: block extents in SGPRs
     float xp[NSUB], yp[NSUB];
     float depth_min[NSUB];
     int best[NSUB];
@@ -429,8 +448,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
                         // faces touching this wave's pixels, walked in ascending order
                         for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
                             const float4* e = s_face + (c0 + __builtin_ctzll(m));
-                            const float4 q0 = e[0], q1 = e[FCAP];
-                            face_test<FCAP>(e, q0, q1, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
+                            FaceRows<FCAP> fr;
+                            fr.load(e);
+                            face_test<FCAP>(e, fr, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
                         }
                     }
                 }

@@ -50,6 +50,9 @@ static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 #ifndef NR_BWD_SKIP_ZERO
 #define NR_BWD_SKIP_ZERO 0  // 1: any all-zero pixel skips the gather (costs the headline ~0.5 %); 0: silhouettes-only renders only
 #endif
+#ifndef NR_BWD_FASTDIV
+#define NR_BWD_FASTDIV 1  // 0: IEEE divisions in the backward's recompute (timing builds)
+#endif
 #ifndef NR_BWD_SKIP_BG
 #define NR_BWD_SKIP_BG 1  // 0: background tiles run the whole kernel (timing builds)
 #endif
@@ -320,9 +323,9 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         // no branch join needs its value: without rgb it reads the face record's first 32 bytes)
         const FaceUV fuv = load_face_uv(rgb ? fuvb + q.fi * 8 : frb + q.fi * FACE_REC);
         __builtin_amdgcn_sched_barrier(0);  // keeps the scheduler from sinking the uv load to its use
-#ifndef NR_BWD_FASTDIV
-        f.flags = 0;  // IEEE divisions here: the shortcut's extra live values cost more than it saves
-#endif
+        // the exact shortened divisions (DESIGN.md "Numerics") as in the forward: bit-identical
+        // values (v28: bwd 0.284 -> 0.279 ms; before the latency fixes of v27-v28 it measured even)
+        if (!NR_BWD_FASTDIV) f.flags = 0;
         bool wfast = false;
         if (NR_ABLATE & 512) {
             q.w[0] = f.x0, q.w[1] = f.y0, q.w[2] = f.z0;  // timing build: no weights
@@ -552,9 +555,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             // silhouettes only: the stencil is zero away from silhouette edges, so only these pixels
             // fetch their face and weights (the same computation as in step 1)
             Face f = load_face_rec(frb + q.fi * FACE_REC);
-#ifndef NR_BWD_FASTDIV
-            f.flags = 0;
-#endif
+            if (!NR_BWD_FASTDIV) f.flags = 0;
             face_weights(xp, pix_center(py, S), f, q.w);
         }
         // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)

@@ -118,20 +118,17 @@ def kernel_bytes(w, args, measured=None):
         "k_shade": fim + frec + (24 * F + T if rgb else 0) + img,
         "k_raster_bwd": fim + img + frec + (24 * F + T + T if rgb else 0) + frec,
         "k_vertex_grad": frec + 4 * (V + 1) + 12 * F + 12 * V * B,
-        "k_tex_out": 2 * T,
+        "k_tex_out": 4 * T // 3 + T,  # read the RGBA accumulator, write the planes
         "k_tex_pack": T + (4 * T // 3 if rgb else 0),  # read the planes, write RGBA rows
     }
-    # the library carries the texture repacking in k_face_setup's idle threads and the texture-gradient
-    # transpose in k_vertex_grad's blocks when they are small (DESIGN.md "Kernels"): their bytes then
-    # count to the carrying kernel
+    # the library carries the texture repacking in k_face_setup's idle threads when it is small
+    # (DESIGN.md "Kernels"): its bytes then count to the carrying kernel
     if measured is not None:
         if "k_shade" not in measured:
             # shading fused into the forward (k_raster_fwd<256, true>): no fim read back
             k["k_raster_fwd"] += k.pop("k_shade") - fim
         if "k_tex_pack" not in measured:
             k["k_face_setup"] += k.pop("k_tex_pack")
-        if "k_tex_out" not in measured:
-            k["k_vertex_grad"] += k.pop("k_tex_out")
     total = B * (8 * S * S + 8 * C * s * s + 36 * V) + 24 * F + (2 * T if T else 0)
     return k, total
 

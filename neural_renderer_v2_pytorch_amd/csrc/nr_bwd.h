@@ -1,4 +1,4 @@
-// nr_bwd.h -- backward: k_raster_bwd, k_vertex_grad, normal backward, k_tex_out, k_param_bwd
+// nr_bwd.h -- backward: k_raster_bwd, k_vertex_grad (lights), normal backward, k_param_bwd
 // Part of nr_raster.hip (one translation unit); see that file and DESIGN.md.
 #pragma once
 
@@ -81,13 +81,19 @@ struct BwdArgs {
     const float* __restrict__ face_records;
     const int32_t* __restrict__ fim;
     const float* __restrict__ grad_images;
-    float* __restrict__ grad_faces;   // [B, F, 9]
-    float* __restrict__ grad_tex4;    // [Bt, HWp, 4] or null
+    float* __restrict__ grad_faces;   // [B, F, 9] face-corner accumulator
+    // texture gradient, two zero-filled accumulators (or null) that k_vertex_grad / k_tex_out add into
+    // the [Bt, 3, H, W] output: RGBA rows [Bt, HWp, 4] for the per-face window flushes (a face's 4x4
+    // window is 4 cache-line rows) and planes [Bt, 3, H, W] for texels outside a face's window (their
+    // three channels on three lines: the RGBA record serialised them on the ShapeNet car's hot texels)
+    float* __restrict__ grad_tex;
+    float* __restrict__ grad_tex_planar;
+    int HWp;
     const float* __restrict__ halo;   // halo cache written by the forward, or null (re-shade the halo)
     const uint8_t* __restrict__ binfg; // per (item, 32x32 bin) foreground flags after the halo values, or null
     float* __restrict__ grad_normals; // [B, F, 9] per-face corner vertex-normal gradients (lights)
     float* __restrict__ grad_bg;      // [B, 3, S, S] or null
-    int F, aa, s, HWp;
+    int F, aa, s, HW;
     float step, inv_step;
     int step_pow2;                     // x / step == x * inv_step exactly
 };
@@ -196,7 +202,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     const int S = g.S;
     const int C = sh.C;
     const bool rgb = !SILO && (sh.draw & NR_DRAW_RGB) != 0;
-    const bool want_tex = rgb && a.grad_tex4 != nullptr;
+    const bool want_tex = rgb && a.grad_tex != nullptr;
     constexpr bool wlate = SILO;  // silhouettes only: weights after the stencil, sparse gather
     int tile_x, tile_y;
     xcd_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(blockIdx.x, b, (S + TW - 1) / TW, (S + BH - 1) / BH, tile_x, tile_y);
@@ -215,7 +221,8 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     const float* __restrict__ frb = a.face_records + (long long)b * a.F * FACE_REC;
     const float* __restrict__ fuvb = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0);
     float* __restrict__ gFb = a.grad_faces + (long long)b * a.F * 9;
-    float* __restrict__ g4b = a.grad_tex4 ? a.grad_tex4 + (long long)bt * a.HWp * 4 : nullptr;
+    float* __restrict__ gtb = a.grad_tex ? a.grad_tex + (long long)bt * 4 * a.HWp : nullptr;
+    float* __restrict__ gtpb = a.grad_tex_planar ? a.grad_tex_planar + (long long)bt * 3 * a.HW : nullptr;
     // wave wid owns the 16x8 block at (16 (wid & 1), 8 (wid >> 1)); lane -> column lane & 15, rows lane >> 4 (+4)
     const int lx = (wid & 1) * 16 + (lane & 15);
     const int ly0 = (wid >> 1) * (4 * NPX) + (lane >> 4);
@@ -399,11 +406,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                     // outside the face window: direct atomics (texel index as sampled)
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        float* gtg = g4b + s.idx[i] * 4;
 #pragma unroll
                         for (int ch = 0; ch < 3; ch++) {
                             const float v = Gt[ch] * s.wt[i];
-                            if (v != 0.f && !(NR_ABLATE & 1024)) unsafeAtomicAdd(gtg + ch, v);
+                            if (v != 0.f && !(NR_ABLATE & 1024)) unsafeAtomicAdd(gtpb + ch * a.HW + s.idx[i], v);
                         }
                     }
                 }
@@ -699,7 +705,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             const bool tex_lane = want_tex && chunk < 3 && sw && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
             const bool face_lane = chunk == 3 && tt < 9;
             const float fv = face_lane ? v : pend;
-            float* dst = tex_lane ? g4b + (y * sh.tv.W + x) * 4 + chunk : gFb + key * 9 + tt;
+            float* dst = tex_lane ? gtb + (y * sh.tv.W + x) * 4 + chunk : gFb + key * 9 + tt;
             if ((tex_lane || face_lane) && fv != 0.f) unsafeAtomicAdd(dst, fv);
             if (win) {
                 pend = sw ? v : pend + v;
@@ -711,7 +717,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     if (!(NR_ABLATE & 4)) {  // the last pending window
         const int x = pwx + tdx, y = pwy + tdy;
         if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
-            unsafeAtomicAdd(g4b + (y * sh.tv.W + x) * 4 + chunk, pend);
+            unsafeAtomicAdd(gtb + (y * sh.tv.W + x) * 4 + chunk, pend);
     }
     NR_TSTAMP(6);
 #ifdef NR_BWD_TIMING
@@ -747,7 +753,7 @@ void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, con
 __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __restrict__ off,
                               const int32_t* __restrict__ ent, float* __restrict__ gV, int F, int V, long long n,
                               TexOut to) {
-    if (to.out) {  // this block's slice of the texture-gradient transpose
+    if (to.out) {  // this block's slice of the texture-gradient output (RGBA window sums + planar rest)
         long long lo, hi;
         grid_slice(to.n, lo, hi);
         for (long long j = lo + threadIdx.x; j < hi; j += blockDim.x) tex_out_one(to, j);
@@ -858,8 +864,8 @@ __global__ void k_fnormal_bwd(const float* __restrict__ face_records, const int3
     o[8] += db2;
 }
 
-// [Bt, HWp, 4] accumulation layout -> [Bt, 3, H, W]
-__global__ void k_tex_out(TexOut to) {  // standalone form (no vertex gradient to carry it)
+// the RGBA texture-gradient accumulator -> [Bt, 3, H, W]
+__global__ void k_tex_out(TexOut to) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < to.n) tex_out_one(to, i);
 }

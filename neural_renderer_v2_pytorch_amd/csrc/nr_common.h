@@ -592,22 +592,15 @@ __device__ __forceinline__ int block_scan(int v, int& total, int* lds4) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Texture repacking, carried by other launches: textures [Bt, 3, H, W] (any strides) -> RGBA rows
-// [Bt, HWp, 4] (alpha slot 0) before the sampling (k_face_setup's idle threads), and the [Bt, HWp, 4]
-// gradient accumulator -> [Bt, 3, H, W] after the backward (k_vertex_grad's blocks).  Each block of
-// the carrying grid takes one contiguous slice, so neither needs a launch of its own.
+// Texture repacking, carried by another launch: textures [Bt, 3, H, W] (any strides) -> RGBA rows
+// [Bt, HWp, 4] (alpha slot 0) before the sampling (k_face_setup's idle threads).  Each block of the
+// carrying grid takes one contiguous slice, so the repacking needs no launch of its own.
 struct TexPack {
     const float* __restrict__ tex;
     long long sb;
     int sc, sp, HW, HWp;
     float4* __restrict__ out;  // null: nothing to pack
     long long n;               // Bt * HWp
-};
-struct TexOut {
-    const float* __restrict__ g4;
-    float* __restrict__ out;   // null: nothing to write
-    int HW, HWp;
-    long long n;               // Bt * HW
 };
 __device__ __forceinline__ void tex_pack_one(const TexPack& pk, long long i) {
     const long long bt = i / pk.HWp;
@@ -619,13 +612,24 @@ __device__ __forceinline__ void tex_pack_one(const TexPack& pk, long long i) {
     }
     pk.out[i] = v;
 }
+// The backward's two texture-gradient accumulators (RGBA rows [Bt, HWp, 4] of the per-face window
+// flushes, planes [Bt, 3, H, W] of the other texels) summed into the [Bt, 3, H, W] gradient, carried by
+// k_vertex_grad's blocks (or k_tex_out)
+struct TexOut {
+    const float* __restrict__ g4;
+    const float* __restrict__ planar;
+    float* __restrict__ out;   // null: nothing to write
+    int HW, HWp;
+    long long n;  // Bt * HW
+};
 __device__ __forceinline__ void tex_out_one(const TexOut& to, long long i) {
     const long long bt = i / to.HW;
     const int p = (int)(i % to.HW);
     const float4 v = reinterpret_cast<const float4*>(to.g4)[bt * to.HWp + p];
-    to.out[(bt * 3 + 0) * to.HW + p] = v.x;
-    to.out[(bt * 3 + 1) * to.HW + p] = v.y;
-    to.out[(bt * 3 + 2) * to.HW + p] = v.z;
+    const float* pl = to.planar + bt * 3 * to.HW + p;
+    to.out[(bt * 3 + 0) * to.HW + p] = v.x + pl[0];
+    to.out[(bt * 3 + 1) * to.HW + p] = v.y + pl[to.HW];
+    to.out[(bt * 3 + 2) * to.HW + p] = v.z + pl[2 * to.HW];
 }
 // this block's slice [lo, hi) of n items spread over the whole grid
 __device__ __forceinline__ void grid_slice(long long n, long long& lo, long long& hi) {

@@ -263,10 +263,13 @@ size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw
            (((size_t)batch_size * g.nbins + 3) & ~size_t(3));
 }
 
+// backward workspace: [gF: B F 9 face-corner floats][g4: Bt HWp RGBA texel rows][planar: Bt 3 H W]
+// [lights: gN: B F 9][gU: B V 3]; everything before gU starts at zero (one memset)
 size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num_vertices, int texture_items,
                                    int tex_height, int tex_width, int num_lights) {
-    const size_t hwp = ((size_t)tex_height * tex_width + 3) & ~size_t(3);
-    size_t n = align_up((size_t)batch_size * num_faces * 9 * 4) + align_up((size_t)texture_items * hwp * 16);
+    const size_t hw = (size_t)tex_height * tex_width, hwp = (hw + 3) & ~size_t(3);
+    size_t n = align_up((size_t)batch_size * num_faces * 9 * 4);
+    if (texture_items > 0) n += align_up((size_t)texture_items * hwp * 16) + align_up((size_t)texture_items * 3 * hw * 4);
     if (num_lights > 0)
         n += align_up((size_t)batch_size * num_faces * 9 * 4) + align_up((size_t)batch_size * num_vertices * 3 * 4);
     return n;
@@ -299,23 +302,26 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     hipStream_t st = (hipStream_t)stream;
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
     const Geom g = make_geom(a->num_faces, S);
-    float* gF = (float*)workspace;
-    const size_t gF_bytes = align_up((size_t)a->batch_size * a->num_faces * 9 * 4);
-    float* g4 = (float*)((char*)workspace + gF_bytes);
     const int HW = a->tex_height * a->tex_width;
     const int HWp = (HW + 3) & ~3;
-    const size_t g4_bytes = align_up((size_t)tex_items * (((size_t)HW + 3) & ~size_t(3)) * 16);
-    float* gN = lit ? (float*)((char*)workspace + gF_bytes + g4_bytes) : nullptr;
-    float* gU = lit ? (float*)((char*)workspace + 2 * gF_bytes + g4_bytes) : nullptr;
+    char* w = (char*)workspace;
+    float* gF = (float*)w;
+    w += align_up((size_t)a->batch_size * a->num_faces * 9 * 4);
+    float* g4 = rgb ? (float*)w : nullptr;
+    float* gpl = rgb ? (float*)(w + align_up((size_t)tex_items * HWp * 16)) : nullptr;
+    if (rgb) w += align_up((size_t)tex_items * HWp * 16) + align_up((size_t)tex_items * 3 * HW * 4);
+    float* gN = lit ? (float*)w : nullptr;
+    float* gU = lit ? (float*)(w + align_up((size_t)a->batch_size * a->num_faces * 9 * 4)) : nullptr;
     // gU is fully written by k_vnormal_bwd; the accumulators before it start at zero
-    const size_t zero_bytes = lit ? 2 * gF_bytes + g4_bytes : need;
+    const size_t zero_bytes = lit ? (size_t)((char*)gU - (char*)workspace) : need;
     if (zero_bytes > 0 && hipMemsetAsync(workspace, 0, zero_bytes, st) != hipSuccess) return check_launch("hipMemsetAsync");
     BwdArgs ba;
     ba.face_records = a->face_records;
     ba.fim = a->face_index;
     ba.grad_images = grad_images;
     ba.grad_faces = gF;
-    ba.grad_tex4 = rgb ? g4 : nullptr;
+    ba.grad_tex = g4;
+    ba.grad_tex_planar = gpl;
     ba.halo = a->halo;
     ba.binfg = a->halo ? (const uint8_t*)a->halo + halo_flags_offset_bytes(a->batch_size, S, nr_num_channels(a->draw_flags))
                        : nullptr;
@@ -324,6 +330,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.F = a->num_faces;
     ba.aa = a->anti_aliasing;
     ba.s = a->image_size;
+    ba.HW = HW;
     ba.HWp = HWp;
     ba.step = (float)(2. / S);
     ba.inv_step = 1.f / ba.step;
@@ -359,14 +366,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
         }
     }
     TexOut to{};
-    if (rgb) {
-        to.g4 = g4;
-        to.out = grad_textures;
-        to.HW = HW;
-        to.HWp = HWp;
-        to.n = (long long)tex_items * HW;
-    }
-    // k_vertex_grad's blocks also carry the texture-gradient transpose when that is a few texels per
+    if (rgb) to = TexOut{g4, gpl, grad_textures, HW, HWp, (long long)tex_items * HW};
+    // k_vertex_grad's blocks also carry the texture-gradient output when that is a few texels per
     // thread; otherwise (no vertices, or a large texture) it gets a launch of its own
     const long long vgrad_threads = (nv + 255) / 256 * 256;
     const bool carry = nv > 0 && to.n <= 8 * vgrad_threads;

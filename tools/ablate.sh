@@ -10,6 +10,8 @@ VARIANTS=${VARIANTS:-base}
 i=0
 for V in $VARIANTS; do
   i=$((i+1))
+  # "lib:<path>": a library built beforehand (e.g. from an older revision, tools/build_rev.sh)
+  if [ "${V#lib:}" != "$V" ]; then cp "${V#lib:}" $OUT/lib/libnr_$i.so || exit 1; continue; fi
   DEFS=""
   if [ "$V" != base ]; then for d in ${V//,/ }; do DEFS="$DEFS -D$d"; done; fi
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math \

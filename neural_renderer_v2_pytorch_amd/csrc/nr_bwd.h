@@ -176,7 +176,7 @@ struct BwdPix {
     float gz[3];       // d/dz of the face corners through the depth and texture-coordinate paths
     float grgb[3];     // upstream gradient of the rgb channels
     float ay, by, ax, bx;
-    int pos;           // bilinear top-left texel relative to the face window: dx | dy << 8; -1 none
+    int pos;           // bilinear top-left texel relative to the face window: dx + 4 dy; -1 none
     int wx, wy;        // face window origin (texels); INT_MIN when not windowed
     float gn[3];       // lights: dL/d(smooth normal)
 };
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                            gx_ < sh.tv.W && gy_ < sh.tv.H;
                 }
                 if (fits) {
-                    q.pos = dx | (dy << 8);
+                    q.pos = dx + 4 * dy;  // window texel of the top-left corner (dx, dy in 0..2)
                 } else {
                     // outside the face window: direct atomics (texel index as sampled)
 #pragma unroll
@@ -584,11 +584,14 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     NR_TSTAMP(4);
 
     // ---- 3. stage this lane's two pixel records; group the wave's records by face --------------
+    // slot of pixel k of lane l: 16 NPX (l >> 4) + 16 k + (l & 15), so member bit b (NPX 16-bit rows)
+    // of chunk c is slot 16 NPX c + b; the first float4 holds the four bilinear corner weights
+    // (ay ax, ay bx, by ax, by bx: the products the accumulation would form)
     float* rec = s_raw + wid * (64 * NPX * REC);
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
-        float* r = rec + (k * 64 + lane) * REC;
-        reinterpret_cast<float4*>(r)[0] = make_float4(P[k].ay, P[k].by, P[k].ax, P[k].bx);
+        float* r = rec + (16 * NPX * (lane >> 4) + 16 * k + (lane & 15)) * REC;
+        reinterpret_cast<float4*>(r)[0] = make_float4(P[k].ay * P[k].ax, P[k].ay * P[k].bx, P[k].by * P[k].ax, P[k].by * P[k].bx);
         reinterpret_cast<float4*>(r)[1] = make_float4(__int_as_float(P[k].pos), P[k].grgb[0], P[k].grgb[1], P[k].grgb[2]);
 #pragma unroll
         for (int j = 0; j < 9; j++) r[8 + j] = gF[k][j];
@@ -658,22 +661,28 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             // this lane's members: row `chunk` of each 16x4 sub-block (lanes 16 chunk .. 16 chunk + 15);
             // bits 0..15 from the first pixel of each lane, 16..31 from the second
             uint32_t mine = ((uint32_t)(m0 >> (16 * chunk)) & 0xffffu) | (((uint32_t)(m1 >> (16 * chunk)) & 0xffffu) << 16);
-            const float* rbase = rec + 16 * chunk * REC;
+            const float* rbase = rec + 16 * NPX * chunk * REC;
             // one member's contribution: its loads issued together, accumulation predicated (no branch)
             auto member = [&](int bit, bool on) {
-                const float* r = rbase + (((bit >> 4) * 64) + (bit & 15)) * REC;
-                const float4 ra = reinterpret_cast<const float4*>(r)[0];  // ay by ax bx
+                const float* r = rbase + bit * REC;
+                const float4 ra = reinterpret_cast<const float4*>(r)[0];  // corner weights w00 w01 w10 w11
                 const float4 rb = reinterpret_cast<const float4*>(r)[1];  // pos G_r G_g G_b
                 const float rf = r[fsel];
+                // whole rows in registers: otherwise the compiler splits the corner select below into
+                // branches, each with its own half-row LDS read
+                asm volatile("" ::"v"(ra.x), "v"(ra.y), "v"(ra.z), "v"(ra.w), "v"(rf));
                 float rw = 0.f, rn = 0.f;
                 if (LIT) {
                     rw = r[nsel_w];
                     rn = r[nsel_n];
                 }
+                // texel tt = tdx + 4 tdy is corner (d & 1, d >> 2) of the member's footprint when
+                // d = tt - pos is 0, 1, 4 or 5 (dx, dy <= 2 rule out row wrap-around)
                 const int pos = __float_as_int(rb.x);
-                const int cx = tdx - (pos & 0xff), cy = tdy - (pos >> 8);
-                const bool hit = on && pos >= 0 && cx >= 0 && cx <= 1 && cy >= 0 && cy <= 1;
-                const float wt = hit ? (cy & 1 ? ra.y : ra.x) * (cx & 1 ? ra.w : ra.z) : 0.f;
+                const int d = tt - pos;
+                const bool hit = on && pos >= 0 && (unsigned)d < 6u && !(d & 2);
+                const float wsel = (d & 4) ? ((d & 1) ? ra.w : ra.z) : ((d & 1) ? ra.y : ra.x);
+                const float wt = hit ? wsel : 0.f;
                 a0 += rb.y * wt;
                 a1 += rb.z * wt;
                 a2 += rb.w * wt;

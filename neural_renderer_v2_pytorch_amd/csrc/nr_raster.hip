@@ -39,6 +39,9 @@
 
 #include "nr_raster.h"
 
+#ifndef NR_VGRAD_BLOCK
+#define NR_VGRAD_BLOCK 256
+#endif
 #ifndef NR_FUSE_SHADE
 #define NR_FUSE_SHADE 1  // 0: k_shade always has its own launch (timing builds)
 #endif
@@ -369,12 +372,13 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     if (rgb) to = TexOut{g4, gpl, grad_textures, HW, HWp, (long long)tex_items * HW};
     // k_vertex_grad's blocks also carry the texture-gradient output when that is a few texels per
     // thread; otherwise (no vertices, or a large texture) it gets a launch of its own
-    const long long vgrad_threads = (nv + 255) / 256 * 256;
+    constexpr int VB = NR_VGRAD_BLOCK;  // small blocks: more of them in flight for this latency-bound gather
+    const long long vgrad_threads = (nv + VB - 1) / VB * VB;
     const bool carry = nv > 0 && to.n <= 8 * vgrad_threads;
     if (nv > 0) {
         {
             ProfScope _p(P_VGRAD, st);
-            hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gF, a->vertex_offsets,
+            hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)((nv + VB - 1) / VB)), dim3(VB), 0, st, gF, a->vertex_offsets,
                                a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv, carry ? to : TexOut{});
         }
         e = check_launch("k_vertex_grad");

@@ -198,14 +198,13 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     __shared__ __attribute__((aligned(16))) float s_raw[bwd_lds<LIT>() / 4];
     float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
     float(*s_G)[HN] = reinterpret_cast<float(*)[HN]>(s_raw + MAXC * HN);
-    const int b = blockIdx.y;
     const int S = g.S;
     const int C = sh.C;
     const bool rgb = !SILO && (sh.draw & NR_DRAW_RGB) != 0;
     const bool want_tex = rgb && a.grad_tex != nullptr;
     constexpr bool wlate = SILO;  // silhouettes only: weights after the stencil, sparse gather
-    int tile_x, tile_y;
-    xcd_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(blockIdx.x, b, (S + TW - 1) / TW, (S + BH - 1) / BH, tile_x, tile_y);
+    int b, tile_x, tile_y;
+    block_item_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(g.group, (S + TW - 1) / TW, (S + BH - 1) / BH, b, tile_x, tile_y);
     const int tx0 = tile_x * TW;
     const int ty0 = tile_y * BH;
     // a tile with no foreground pixel contributes nothing (every gradient term is per foreground

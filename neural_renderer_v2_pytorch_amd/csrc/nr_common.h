@@ -15,7 +15,14 @@ constexpr int COARSE = 32;         // coarse bin edge (pixels) = forward block r
 #endif
 constexpr int SETUP_FACES = NR_SETUP_FACES;  // faces per setup block (SETUP_FACES / 32 bitmask words)
 static_assert(SETUP_FACES % 32 == 0 && SETUP_FACES <= 256, "setup block layout");
-constexpr int SETUP_LDS_WORDS = 4096;  // bin-mask words built in LDS (up to 1024 bins, S <= 1024)
+constexpr int SETUP_LDS_WORDS = 12288;  // bin-mask words built in LDS (dynamic LDS, 48 KB: 2048 bins, S <= 1448, at 192 faces)
+// dynamic LDS words of a k_face_setup launch: the staged face records, or the block's mask words of
+// every bin when those fit SETUP_LDS_WORDS (else the setup tests every (bin, word) from global memory)
+inline int setup_lds_words(int nbins) {
+    const int m = nbins * (SETUP_FACES / 32);
+    const int stage = SETUP_FACES * 16;  // FACE_REC
+    return (m <= SETUP_LDS_WORDS && m > stage) ? m : stage;
+}
 constexpr int MAXC = 5;            // max output channels
 
 thread_local std::string g_err;
@@ -63,6 +70,7 @@ struct ProfScope {  // records the start/end events of one launch when profiling
 
 struct Geom {
     int S, nbx, nby, nbins, nwords, tiles_x, tiles_y;
+    int group;  // item-interleave group of the raster launches (block_item_tile); 0: per-item bands
 };
 
 Geom make_geom(int F, int S) {
@@ -74,6 +82,7 @@ Geom make_geom(int F, int S) {
     g.nwords = (F + 31) / 32;
     g.tiles_x = (S + TW - 1) / TW;
     g.tiles_y = (S + TH - 1) / TH;
+    g.group = 0;
     return g;
 }
 
@@ -565,6 +574,47 @@ __device__ __forceinline__ void xcd_tile(int L, int b, int nx, int ny, int& tx, 
         }
     }
 }
+
+// The (item, tile) of a raster block.  group 0: item = blockIdx.y, tile by xcd_tile (bands per XCD,
+// rotating with the item).  group G > 0 (G % 8 == 0, B % G == 0): items interleaved in groups of G:
+// the linear block id L = blockIdx.y gridDim.x + blockIdx.x (the dispatch order) runs over groups of
+// G items, and within a group over the tiles in row-major order with the item fastest (item = group
+// G + L % G).  Workgroups go to XCD L % 8 = item % 8, so an XCD keeps its items' face records in its
+// own L2; and the last blocks dispatched are the last group's last tile rows -- background for a
+// centred object -- so a kernel does not end on a tail of foreground tiles that started last (a
+// foreground bin's waves live ~7x longer than a background bin's).  Smaller groups put fewer items on
+// the same tile at once, which matters to the backward's atomics into a shared texture's hot texels.
+// (group_for picks G on the host.)
+template <int MODE, int SW_, int SH>
+__device__ __forceinline__ void block_item_tile(int G, int nx, int ny, int& b, int& tx, int& ty) {
+    if (G > 0) {
+        const int L = blockIdx.y * gridDim.x + blockIdx.x;
+        const int per = G * gridDim.x;  // blocks per group
+        const int grp = L / per, r = L - grp * per;
+        b = grp * G + r % G;
+        const int t = r / G;
+        tx = t % nx;
+        ty = t / nx;
+        return;
+    }
+    b = blockIdx.y;
+    xcd_tile<MODE, SW_, SH>(blockIdx.x, b, nx, ny, tx, ty);
+}
+// the interleave group for B items and a preferred group size: the preference when it divides B, else
+// all B items; 0 (per-item bands) when B is not a multiple of 8
+inline int group_for(int B, int pref) {
+    if (pref <= 0 || B % 8 != 0) return 0;
+    return B % pref == 0 ? pref : B;
+}
+#ifndef NR_FWD_GROUP
+#define NR_FWD_GROUP 64
+#endif
+#ifndef NR_BWD_GROUP
+#define NR_BWD_GROUP 64
+#endif
+#ifndef NR_BWD_GROUP_TEX
+#define NR_BWD_GROUP_TEX 16  // a shared texture: fewer items on a tile at once (hot-texel atomics)
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // block-wide exclusive scan of one int per thread (NW waves)

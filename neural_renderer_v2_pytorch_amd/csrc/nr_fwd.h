@@ -22,8 +22,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
     __shared__ int2 s_bb[SETUP_FACES];
     // the block's face records, assembled per face and then written out coalesced (a record per lane
     // would store 64-B strided rows); the bin-mask words reuse the space afterwards
-    constexpr int STAGE = SETUP_FACES * FACE_REC;
-    __shared__ __attribute__((aligned(16))) float s_stage[STAGE > SETUP_LDS_WORDS ? STAGE : SETUP_LDS_WORDS];
+    extern __shared__ __attribute__((aligned(16))) float s_stage[];  // setup_lds_words(nbins) floats
     float* s_frec = s_stage;
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_stage);
     const int b = blockIdx.y;
@@ -128,7 +127,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
     // coarse-bin bitmask words of this face group
     const int w0 = blockIdx.x * (SETUP_FACES / 32);
     const int nw = min(SETUP_FACES / 32, nwords - w0);
-    if (nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS) {
+    if (nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS) {  // (setup_lds_words sized s_stage for this)
         // each face sets its bit in the (few) bins its pixel range touches (LDS ds_or), then the
         // block writes its words out
         for (int i = t; i < nbins * (SETUP_FACES / 32); i += blockDim.x) s_mask[i] = 0u;
@@ -377,10 +376,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     float4* s_face = reinterpret_cast<float4*>(s_raw);
     int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
 
-    const int b = blockIdx.y;
     const int S = g.S;
-    int bin_x, bin_y;
-    xcd_tile<NR_FSWZ_MODE, NR_FSWZ_W, NR_FSWZ_H>(blockIdx.x, b, g.nbx, g.nby, bin_x, bin_y);
+    int b, bin_x, bin_y;
+    block_item_tile<NR_FSWZ_MODE, NR_FSWZ_W, NR_FSWZ_H>(g.group, g.nbx, g.nby, b, bin_x, bin_y);
     const int bin = bin_y * g.nbx + bin_x;
     const int bx0 = bin_x * COARSE;
     const int by0 = bin_y * COARSE;

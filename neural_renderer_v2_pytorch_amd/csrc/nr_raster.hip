@@ -88,14 +88,15 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                           int B, int V, int F, int S, float near, float far, int draw_backside, float delta,
                           void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images,
                           TexPack pk) {
-    const Geom g = make_geom(F, S);
+    Geom g = make_geom(F, S);
+    g.group = group_for(B, NR_FWD_GROUP);
     int2* bbox = (int2*)ws;
     uint32_t* mask = (uint32_t*)((char*)ws + ws_bbox_bytes(B, F));
     if (B == 0) return NR_OK;
-    // the setup's idle threads repack the textures when that takes them a few texels each; with no
+    // the setup's idle threads repack the textures when that takes them up to 32 texels each; with no
     // setup launch, or a texture too large for that, the repacking gets a launch of its own
     const long long setup_idle = (long long)((F + SETUP_FACES - 1) / SETUP_FACES) * B * (256 - SETUP_FACES);
-    if (pk.out && (F == 0 || pk.n > 8 * setup_idle)) {
+    if (pk.out && (F == 0 || pk.n > 32 * setup_idle)) {
         ProfScope _p(P_TEXPACK, st);
         hipLaunchKernelGGL(k_tex_pack, dim3((unsigned)((pk.n + 255) / 256)), dim3(256), 0, st, pk);
         const int e = check_launch("k_tex_pack");
@@ -108,14 +109,15 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         const int uv_items = rgb ? (ra->vt_batch_stride ? B : 1) : 0;
         ProfScope _p(P_SETUP, st);
         const bool lit = rgb && ra->num_lights > 0;
+        const size_t lds = (size_t)setup_lds_words(g.nbins) * 4;
         if (vertices)
-            hipLaunchKernelGGL(k_face_setup<true>, grid, dim3(256), 0, st, vertices, faces_idx, face_records, V, F, S,
+            hipLaunchKernelGGL(k_face_setup<true>, grid, dim3(256), lds, st, vertices, faces_idx, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
                                rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk);
         else
-            hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), 0, st, nullptr, nullptr, face_records, V, F, S,
+            hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
                                nullptr, pk);
         int e = check_launch("k_face_setup");
@@ -304,7 +306,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
         return fail(NR_ERR_WORKSPACE, "backward workspace missing or too small");
     hipStream_t st = (hipStream_t)stream;
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
-    const Geom g = make_geom(a->num_faces, S);
+    Geom g = make_geom(a->num_faces, S);
+    g.group = group_for(a->batch_size, rgb && !a->tex_stride_b ? NR_BWD_GROUP_TEX : NR_BWD_GROUP);
     const int HW = a->tex_height * a->tex_width;
     const int HWp = (HW + 3) & ~3;
     char* w = (char*)workspace;

@@ -198,7 +198,9 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //      and walks the set bits in order (scalar loop), running the reference's per-face test for its
 //      pixel -- every pixel therefore sees its candidate faces in ascending index order, as the
 //      reference's sequential loop does (.cu:82-149), and the per-pixel state stays in registers
-//      across rounds;
+//      across rounds; the test is split into a per-face pass test and a deferred commit
+//      (NR_FWD_DEFER), and the deep-bin variant first drops faces whose edge tests fail over the
+//      whole 8x8 block (block_culled, NR_FWD_CULL);
 //   shading and the output image are computed by k_shade.
 //   Block sizes (picked per launch, run_face_index): 256 threads = 4 waves, each walking the four 8x8
 //   blocks of a 16x16 quadrant (most per-thread work, least fixed cost per pixel: best when the grid
@@ -316,6 +318,104 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
     }
 }
 
+// The deferred form of face_test (NR_FWD_DEFER): the walk runs only the state-independent part of
+// the test per face (face_pass), and keeps per pixel the one face that passed it and is not yet
+// committed; the rest of the test -- depth reject, barycentric division chain, near / far and the
+// z-test (face_commit) -- runs for all pending pixels of the wave at once, when a newly walked face
+// passes at a pixel that already has a pending face, and at the end of the block's walk. Every pixel
+// still commits its faces in ascending order with the state the sequential loop has at that point
+// (what was pending has been committed before), so the result is that of .cu:82-149; the division
+// chain, run by the whole wave for any one passing lane, runs about a third as often on the headline.
+#ifndef NR_FWD_DEFER
+#define NR_FWD_DEFER 1
+#endif
+// .cu:94-116, with the depth reject of .cu:124-126 against depth_bound >= the pixel's current
+// minimum (a face it rejects the exact test rejects too); rows 0-5 of the record
+template <int FST>
+__device__ __forceinline__ bool face_pass(const float4* e, const FaceRows<FST>& fr, float xp, float yp, float depth_bound) {
+    const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1);
+    if (depth_bound < q1.z) return false;
+    if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return false;
+    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4), q5 = fr.get(e, 5);
+    const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
+    const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
+    const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
+    if (c1 * c2 < 0) return false;
+    const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
+    return !(c2 * c3 < 0);
+}
+// .cu:124-148 for a face that passed face_pass at this pixel (e: its record, a per-lane address)
+template <int FST>
+__device__ __forceinline__ void face_commit(const float4* e, float xp, float yp, float near, float far, float delta,
+                                            float& depth_min, int& best) {
+    const float4 q1 = e[1 * FST];
+    if (depth_min < q1.z) return;
+    const float4 q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST], q7 = e[7 * FST];
+    const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
+    float w0 = (yp * q4.w - xp * q5.x) + q5.w;
+    float w1 = (yp * q5.y - xp * q5.z) + q6.x;
+    float w2 = (yp * q4.y - xp * q4.z) + q6.y;
+    const float ws = w0 + w1 + w2;
+    float zp;
+    if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {  // as face_test
+        const float rs = rcp_nr(ws);
+        w0 = div_nr(w0, ws, rs);
+        w1 = div_nr(w1, ws, rs);
+        w2 = div_nr(w2, ws, rs);
+        const float sum = div_nr(w0, z0, q6.z) + div_nr(w1, z1, q6.w) + div_nr(w2, z2, q7.x);
+        if (in_range(sum, 0x1p-90f, 0x1p90f)) {
+            const float r = rcp_nr(sum);
+            zp = __builtin_fmaf(__builtin_fmaf(-sum, r, 1.f), r, r);
+            zp = __builtin_fmaf(__builtin_fmaf(-sum, zp, 1.f), r, zp);
+        } else {
+            zp = 1.f / sum;
+        }
+    } else {
+        w0 /= ws;
+        w1 /= ws;
+        w2 /= ws;
+        zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
+    }
+    if (zp <= near || far <= zp) return;
+    if (zp <= depth_min - delta) {
+        depth_min = zp;
+        best = __float_as_int(q1.w);
+    }
+}
+
+// Edge cull of a staged face against an 8x8 block (NR_FWD_CULL, deep-bin variant): true only when
+// the reference's edge tests (.cu:107-116) fail at every pixel centre of the block. Edge k's
+// function c_k is affine in the pixel, so its range over the block is centre +- half-range; a sign
+// is trusted when the whole range clears a margin covering the rounding of the reference's own float
+// evaluation and of this one (2^-18 of the magnitude bound T, at least 2^-60 so that a product of
+// two trusted values cannot underflow to 0). The tests fail at a pixel when c1 c2 < 0 or c2 c3 < 0,
+// so the block is culled when c1, c2 or c2, c3 have trusted opposite signs, or c1, c3 do and c2 has
+// a trusted sign (with c2 exactly 0 the reference passes the pixel whatever c1 and c3 are). NaN and
+// infinite operands never produce a trusted sign.
+#ifndef NR_FWD_CULL
+#define NR_FWD_CULL 1
+#endif
+__device__ __forceinline__ void edge_sign(float ax, float ay, float A, float B, float xc, float yc, float hx, float hy,
+                                          bool& pos, bool& neg) {
+    const float dy = yc - ay, dx = xc - ax;
+    const float cc = dy * A - B * dx;
+    const float aA = fabsf(A), aB = fabsf(B);
+    const float hr = hy * aA + hx * aB;
+    const float T = (fabsf(yc) + fabsf(ay) + hy) * aA + (fabsf(xc) + fabsf(ax) + hx) * aB;
+    const float m = fmaxf(T * 0x1p-18f, 0x1p-60f) + hr;
+    pos = cc > m;
+    neg = cc < -m;
+}
+template <int FST>
+__device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc, float hx, float hy) {
+    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
+    bool p1, n1, p2, n2, p3, n3;
+    edge_sign(q2.x, q2.y, q4.y, q4.z, xc, yc, hx, hy, p1, n1);  // c1: (x0, y0), A = x1 - x0, B = y1 - y0
+    edge_sign(q2.z, q2.w, q4.w, q5.x, xc, yc, hx, hy, p2, n2);  // c2: (x1, y1), C, D
+    edge_sign(q3.x, q3.y, q5.y, q5.z, xc, yc, hx, hy, p3, n3);  // c3: (x2, y2), E, F
+    return (p1 && n2) || (n1 && p2) || (p2 && n3) || (n2 && p3) || (((p1 && n3) || (n1 && p3)) && (p2 || n2));
+}
+
 template <int FST>
 __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f, int2 bb) {
     const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
@@ -342,7 +442,7 @@ __device__ unsigned long long g_fwd_t[NR_FTIMING_MAX];
     do {                                                                                                   \
         const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 8 + (k); \
         const unsigned long long t_ = (v);                                                                 \
-        if (SHADE && (threadIdx.x & 63) == 0 && i_ < NR_FTIMING_MAX) g_fwd_t[i_] = t_;                       \
+        if ((threadIdx.x & 63) == 0 && i_ < NR_FTIMING_MAX) g_fwd_t[i_] = t_;                       \
     } while (0)
 #else
 #define NR_FTSTAMP(k, v) \
@@ -371,6 +471,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || (NTF == 256 && COARSE == 32), "fused shading: one output pixel per thread");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
+    constexpr bool CULL = NR_FWD_CULL && NTF >= 1024;  // deep bins: small faces over each 8x8 block
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
     __shared__ int s_scan[C::NW];
     float4* s_face = reinterpret_cast<float4*>(s_raw);
@@ -408,6 +509,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     int32_t* __restrict__ fimb = fim + (long long)b * S * S;
 
     NR_FTSTAMP(0, clock64());
+#ifdef NR_FWD_TIMING
+    unsigned long long t_stage = 0;
+#endif
     int ncand = 0;  // the bin's candidate faces (block-uniform)
     for (int wbase = 0; wbase < g.nwords; wbase += NTF) {
         const int w = wbase + t;
@@ -428,29 +532,57 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
             const int nc = min(CAND, total - cbase);
             for (int j0 = 0; j0 < nc; j0 += FCAP) {
                 const int n = min(FCAP, nc - j0);
+#ifdef NR_FWD_TIMING
+                const unsigned long long ts0_ = clock64();
+#endif
                 if (t < n) {
                     const int f = s_cand[j0 + t];
                     stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
                 }
                 __syncthreads();
-                NR_FTSTAMP(2, clock64());
+#ifdef NR_FWD_TIMING
+                t_stage += clock64() - ts0_;  // staging rounds (the expansion is in the walk's share)
+#endif
 #pragma unroll
                 for (int k = 0; k < NSUB; k++) {
                     const float xc0 = xcl[k], xc1 = xch[k], yc0 = ycl[k], yc1 = ych[k];
+#if NR_FWD_DEFER
+                    int pend = -1;                // staging slot of my pixel's pending face
+                    unsigned long long occ = 0;   // the wave's pixels with a pending face
+#endif
                     for (int c0 = 0; c0 < n; c0 += 64) {
                         bool hit = false;
                         if (c0 + lane < n) {
                             const float4 q0 = s_face[c0 + lane];
                             hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
+                            if (CULL && hit)
+                                hit = !block_culled<FCAP>(s_face + c0 + lane, 0.5f * (xc0 + xc1), 0.5f * (yc0 + yc1),
+                                                          0.5f * (xc1 - xc0), 0.5f * (yc1 - yc0));
                         }
                         // faces touching this wave's pixels, walked in ascending order
                         for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
-                            const float4* e = s_face + (c0 + __builtin_ctzll(m));
+                            const int slot = c0 + __builtin_ctzll(m);
+                            const float4* e = s_face + slot;
                             FaceRows<FCAP> fr;
                             fr.load(e);
+#if NR_FWD_DEFER
+                            const bool pass = face_pass<FCAP>(e, fr, xp[k], yp[k], depth_min[k]);
+                            const unsigned long long cov = __ballot(pass);
+                            if (cov & occ) {  // commit first where this face would queue behind a pending one
+                                if (pend >= 0) face_commit<FCAP>(s_face + pend, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
+                                pend = -1;
+                                occ = 0;
+                            }
+                            if (pass) pend = slot;
+                            occ |= cov;
+#else
                             face_test<FCAP>(e, fr, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
+#endif
                         }
                     }
+#if NR_FWD_DEFER
+                    if (pend >= 0) face_commit<FCAP>(s_face + pend, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
+#endif
                 }
                 __syncthreads();
             }
@@ -458,6 +590,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     }
 
     NR_FTSTAMP(3, clock64());
+    NR_FTSTAMP(2, t_stage);
 #pragma unroll
     for (int k = 0; k < NSUB; k++) {
         int ox, oy;
@@ -468,6 +601,11 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     // may the bin hold a foreground pixel (the backward skips its tiles when not): a bin without
     // candidate faces holds none
     if (binfg && t == 0) binfg[(long long)b * g.nbins + bin] = ncand > 0 ? 1 : 0;
+    if (!SHADE) {
+        NR_FTSTAMP(4, clock64());
+        NR_FTSTAMP(5, clock64());
+        NR_FTSTAMP(6, (unsigned long long)ncand);
+    }
     if (SHADE && ncand == 0) {
         // an empty bin: every channel of its output pixels is 0 (sil, depth and rgb of background;
         // no backgrounds in this variant), as is every halo value

@@ -135,7 +135,8 @@ def cfg2(dev, a):
     return res
 
 
-def cfg3(dev, a):
+def cfg3_step(dev):
+    """The car scene and its fwd+bwd step (also used by tools/fwd_timing.py --workload car)."""
     v, f, vt, ft, tex = nr.load_obj(os.path.join(DATA, "4e49873292196f02574b5684eaec43e9", "model.obj"),
                                     load_textures=True)
     v, f, vt, ft = subdivide(v, f, vt, ft)
@@ -153,6 +154,11 @@ def cfg3(dev, a):
     def step():
         proj.grad = tex.grad = None
         nr.rasterize_rgba(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
+    return step, f, B, s
+
+
+def cfg3(dev, a):
+    step, f, B, s = cfg3_step(dev)
     t = median_step(step, a.steps, a.warmup)
     return dict(config="cfg3 car (1x subdivided) B=64 256^2 textured rgba", faces=int(f.shape[0]), batch=B,
                 image_size=s, ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),

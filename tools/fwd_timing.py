@@ -1,7 +1,8 @@
-"""Per-wave phase timing of the fused forward k_raster_fwd<256, true> on the headline workload
-(timing build, NR_FWD_TIMING).  usage (GPU box): python tools/fwd_timing.py [extra -D flags...]
-Phases: mask words + candidate scan, candidate expansion + face staging, face walk, fim write + bin
-flag + LDS hand-over, shading epilogue; split by the bin's candidate count."""
+"""Per-wave phase timing of the forward k_raster_fwd on the headline workload (the fused <256, true>
+variant) or the car (--workload car: <1024, false>; no shading phase) (timing build, NR_FWD_TIMING).
+usage (GPU box): python tools/fwd_timing.py [--workload car] [extra -D flags...]
+Phases: mask words + candidate scan, face staging rounds (summed), candidate expansion + face walk,
+fim write + bin flag + LDS hand-over, shading epilogue; split by the bin's candidate count."""
 import ctypes
 import os
 import subprocess
@@ -11,6 +12,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 lib_path = "/tmp/libnr_ftiming.so"
+WORKLOAD = "headline"
+if len(sys.argv) > 2 and sys.argv[1] == "--workload":
+    WORKLOAD = sys.argv[2]
+    del sys.argv[1:3]
 subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                        "-ffp-contract=off", "-fno-fast-math", "-fvisibility=hidden", "-DNR_FWD_TIMING", "-I" + ROOT + "/include"]
                       + sys.argv[1:] + [ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib_path])
@@ -20,23 +25,33 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 sys.argv = [sys.argv[0]]
-args = bench.parse()
 torch.cuda.set_device(0)
-w = bench.workload(args, 0, torch.device("cuda", 0))
+if WORKLOAD == "car":
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs  # noqa: E402
+    step, _, batch, size = bench_configs.cfg3_step(torch.device("cuda", 0))
+    waves = 16  # deep bins: the 1024-thread variant
+else:
+    args = bench.parse()
+    w = bench.workload(args, 0, torch.device("cuda", 0))
+    batch, size, waves = args.batch, args.image_size, 4
+
+    def step():
+        bench.step(w)
 for _ in range(4):
-    bench.step(w)
+    step()
 torch.cuda.synchronize()
 from neural_renderer_v2_pytorch_amd import _lib  # noqa: E402
 L = _lib.lib()
-S = 2 * args.image_size
-blocks = (S // 32) ** 2 * args.batch
-n = blocks * 4 * 8
+S = 2 * size
+blocks = (S // 32) ** 2 * batch
+n = blocks * waves * 8
 buf = (ctypes.c_ulonglong * n)()
 assert L.nr_debug_fwd_timing(buf, ctypes.c_size_t(n)) == 0
-t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(blocks, 4, 8)
+t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(blocks, waves, 8)
 nc = t[:, 0, 6]
-t2 = np.where((nc > 0)[:, None], t[:, :, 2], t[:, :, 1])  # no staging stamp without candidates
-ph = np.stack([t[:, :, 1] - t[:, :, 0], t2 - t[:, :, 1], t[:, :, 3] - t2,
+st = t[:, :, 2]  # cycles in the staging rounds (face loads + LDS stores + barrier), summed
+ph = np.stack([t[:, :, 1] - t[:, :, 0], st, t[:, :, 3] - t[:, :, 1] - st,
                t[:, :, 4] - t[:, :, 3], t[:, :, 5] - t[:, :, 4]], axis=2)
 names = ["scan", "stage", "walk", "fim+flag", "shade"]
 life = t[:, :, 5] - t[:, :, 0]

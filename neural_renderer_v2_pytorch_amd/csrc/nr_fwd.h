@@ -217,7 +217,7 @@ template <int NTF> struct FwdCfg {
     static constexpr int NW = NTF / 64;                        // waves
     static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
     static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
-    static constexpr int FCAP = NTF >= 1024 ? 256 : 128;       // faces staged per round
+    static constexpr int FCAP = NTF >= 512 ? 256 : 128;        // faces staged per round
     static constexpr int LDS = FCAP * FREC * 16 + CAND * 4;
     static_assert(NSUB == 1 || NSUB == 2 || NSUB == 4, "forward block layout");
     // 8x8 block k of wave w: its origin (ox, oy) in the bin
@@ -329,6 +329,9 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
 #ifndef NR_FWD_DEFER
 #define NR_FWD_DEFER 1
 #endif
+#ifndef NR_FWD_DYN
+#define NR_FWD_DYN NR_FWD_DEFER  // single-round bins deal their 8x8 blocks out to the waves (k_raster_fwd)
+#endif
 // .cu:94-116, with the depth reject of .cu:124-126 against depth_bound >= the pixel's current
 // minimum (a face it rejects the exact test rejects too); rows 0-5 of the record
 template <int FST>
@@ -344,10 +347,12 @@ __device__ __forceinline__ bool face_pass(const float4* e, const FaceRows<FST>& 
     const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
     return !(c2 * c3 < 0);
 }
-// .cu:124-148 for a face that passed face_pass at this pixel (e: its record, a per-lane address)
-template <int FST>
-__device__ __forceinline__ void face_commit(const float4* e, float xp, float yp, float near, float far, float delta,
-                                            float& depth_min, int& best) {
+// .cu:124-148 for a face that passed face_pass at this pixel (slot: its staging slot, per lane);
+// the winner is recorded as its face id, or (SLOT) as its staging slot
+template <int FST, bool SLOT>
+__device__ __forceinline__ void face_commit(const float4* s_face, int slot, float xp, float yp, float near, float far,
+                                            float delta, float& depth_min, int& best) {
+    const float4* e = s_face + slot;
     const float4 q1 = e[1 * FST];
     if (depth_min < q1.z) return;
     const float4 q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST], q7 = e[7 * FST];
@@ -379,7 +384,7 @@ __device__ __forceinline__ void face_commit(const float4* e, float xp, float yp,
     if (zp <= near || far <= zp) return;
     if (zp <= depth_min - delta) {
         depth_min = zp;
-        best = __float_as_int(q1.w);
+        best = SLOT ? slot : __float_as_int(q1.w);
     }
 }
 
@@ -414,6 +419,52 @@ __device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc
     edge_sign(q2.z, q2.w, q4.w, q5.x, xc, yc, hx, hy, p2, n2);  // c2: (x1, y1), C, D
     edge_sign(q3.x, q3.y, q5.y, q5.z, xc, yc, hx, hy, p3, n3);  // c3: (x2, y2), E, F
     return (p1 && n2) || (n1 && p2) || (p2 && n3) || (n2 && p3) || (((p1 && n3) || (n1 && p3)) && (p2 || n2));
+}
+
+// one wave's walk of the n staged faces over its 8x8 block (pixel (xp, yp) per lane, pixel-centre
+// extent [xc0, xc1] x [yc0, yc1]): bbox ballot (+ edge cull), then the per-face test in ascending order
+template <int FST, bool CULL, bool SLOT>
+__device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, int n, int lane, float xp, float yp,
+                                           float xc0, float xc1, float yc0, float yc1, float near, float far,
+                                           float delta, float& depth_min, int& best) {
+#if NR_FWD_DEFER
+    int pend = -1;               // staging slot of my pixel's pending face
+    unsigned long long occ = 0;  // the wave's pixels with a pending face
+#endif
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        bool hit = false;
+        if (c0 + lane < n) {
+            const float4 q0 = s_face[c0 + lane];
+            hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
+            if (CULL && hit)
+                hit = !block_culled<FST>(s_face + c0 + lane, 0.5f * (xc0 + xc1), 0.5f * (yc0 + yc1), 0.5f * (xc1 - xc0),
+                                         0.5f * (yc1 - yc0));
+        }
+        // faces touching this wave's pixels, walked in ascending order
+        for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
+            const int slot = c0 + __builtin_ctzll(m);
+            const float4* e = s_face + slot;
+            FaceRows<FST> fr;
+            fr.load(e);
+#if NR_FWD_DEFER
+            const bool pass = face_pass<FST>(e, fr, xp, yp, depth_min);
+            const unsigned long long cov = __ballot(pass);
+            if (cov & occ) {  // commit first where this face would queue behind a pending one
+                if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
+                pend = -1;
+                occ = 0;
+            }
+            if (pass) pend = slot;
+            occ |= cov;
+#else
+            static_assert(!SLOT, "slot-recording walks need NR_FWD_DEFER");
+            face_test<FST>(e, fr, xp, yp, near, far, delta, depth_min, best);
+#endif
+        }
+    }
+#if NR_FWD_DEFER
+    if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
+#endif
 }
 
 template <int FST>
@@ -471,9 +522,10 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || (NTF == 256 && COARSE == 32), "fused shading: one output pixel per thread");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
-    constexpr bool CULL = NR_FWD_CULL && NTF >= 1024;  // deep bins: small faces over each 8x8 block
+    constexpr bool CULL = NR_FWD_CULL && NTF >= 512;  // deep bins: small faces over each 8x8 block
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
     __shared__ int s_scan[C::NW];
+    __shared__ int s_next;  // (dyn) next 8x8 block to walk
     float4* s_face = reinterpret_cast<float4*>(s_raw);
     int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
 
@@ -485,23 +537,6 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     const int by0 = bin_y * COARSE;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: block extents in SGPRs
-    float xp[NSUB], yp[NSUB];
-    float depth_min[NSUB];
-    int best[NSUB];
-    float xcl[NSUB], xch[NSUB], ycl[NSUB], ych[NSUB];
-#pragma unroll
-    for (int k = 0; k < NSUB; k++) {
-        int ox, oy;
-        C::block_of(wid, k, ox, oy);
-        xcl[k] = pix_center(bx0 + ox, S);
-        xch[k] = pix_center(bx0 + ox + 7, S);
-        ycl[k] = pix_center(by0 + oy, S);
-        ych[k] = pix_center(by0 + oy + 7, S);
-        xp[k] = pix_center(bx0 + ox + (lane & 7), S);
-        yp[k] = pix_center(by0 + oy + (lane >> 3), S);
-        depth_min[k] = far;
-        best[k] = -1;
-    }
 
     const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
     const int2* bbb = bbox + (long long)b * F;
@@ -512,92 +547,146 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
 #ifdef NR_FWD_TIMING
     unsigned long long t_stage = 0;
 #endif
+    // the first round of mask words and its candidate count
+    const uint32_t bits0 = (t < g.nwords) ? words[t] : 0u;
+    int total0;
+    const int off0 = block_scan<C::NW>(__builtin_popcount(bits0), total0, s_scan);
+    NR_FTSTAMP(1, clock64());
+    // one staging round holds every candidate of the bin (the usual case): the waves take the 16 8x8
+    // blocks one at a time from a counter, so a wave that meets few faces goes on to another block
+    // instead of idling at the block's end (static quadrants keep 80 % of the waves' time busy on the
+    // headline, dealt blocks ~92 %, CPU-counted; measured fwd 0.212 -> 0.208 ms)
+    // (not with 16 waves: one block each already; measured 0.824 -> 0.918 ms on the car)
+    const bool dyn = NR_FWD_DYN && NTF < 1024 && g.nwords <= NTF && total0 <= FCAP;
     int ncand = 0;  // the bin's candidate faces (block-uniform)
-    for (int wbase = 0; wbase < g.nwords; wbase += NTF) {
-        const int w = wbase + t;
-        const uint32_t bits = (w < g.nwords) ? words[w] : 0u;
-        int total;
-        const int off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
-        ncand += total;
-        NR_FTSTAMP(1, clock64());
-        for (int cbase = 0; cbase < total; cbase += CAND) {
-            // expand my word's set bits into the ordered candidate list
-            int r = off;
-            for (uint32_t m = bits; m; m &= m - 1, r++) {
-                if (r < cbase) continue;
-                if (r >= cbase + CAND) break;
-                s_cand[r - cbase] = w * 32 + __builtin_ctz(m);
+    unsigned short* s_slot = reinterpret_cast<unsigned short*>(s_cand);  // (dyn, SHADE) winners' staging slots
+    static_assert(!SHADE || CAND * 4 >= COARSE * COARSE * 2, "slot map in the candidate list's space");
+    if (dyn) {
+        ncand = total0;
+        if (ncand == 0) {
+            for (int u = wid; u < 16; u += C::NW) {
+                const int px = bx0 + (u & 3) * 8 + (lane & 7), py = by0 + (u >> 2) * 8 + (lane >> 3);
+                if (px < S && py < S) fimb[py * S + px] = -1;
+            }
+        } else {
+            int r = off0;
+            for (uint32_t m = bits0; m; m &= m - 1, r++) s_cand[r] = t * 32 + __builtin_ctz(m);
+            if (t == 0) s_next = 0;
+            __syncthreads();
+#ifdef NR_FWD_TIMING
+            const unsigned long long ts0_ = clock64();
+#endif
+            if (t < ncand) {
+                const int f = s_cand[t];
+                stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
             }
             __syncthreads();
-            const int nc = min(CAND, total - cbase);
-            for (int j0 = 0; j0 < nc; j0 += FCAP) {
-                const int n = min(FCAP, nc - j0);
 #ifdef NR_FWD_TIMING
-                const unsigned long long ts0_ = clock64();
+            t_stage += clock64() - ts0_;
 #endif
-                if (t < n) {
-                    const int f = s_cand[j0 + t];
-                    stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
+            for (;;) {
+                int u = 0;
+                if (lane == 0) u = atomicAdd(&s_next, 1);
+                u = __builtin_amdgcn_readfirstlane(u);  // lane 0's value: the wave is whole here
+                if (u >= 16) break;
+                const int ox = (u & 3) * 8, oy = (u >> 2) * 8;
+                float depth_min = far;
+                int best = -1;
+                walk_block<FCAP, CULL, SHADE>(s_face, ncand, lane, pix_center(bx0 + ox + (lane & 7), S),
+                                              pix_center(by0 + oy + (lane >> 3), S), pix_center(bx0 + ox, S),
+                                              pix_center(bx0 + ox + 7, S), pix_center(by0 + oy, S),
+                                              pix_center(by0 + oy + 7, S), near, far, delta, depth_min, best);
+                int id = best;
+                if (SHADE) {  // best is the staging slot: its face id is in the record's row 1
+                    id = best >= 0 ? __float_as_int(s_face[FCAP + best].w) : -1;
+                    s_slot[(oy + (lane >> 3)) * COARSE + ox + (lane & 7)] = best >= 0 ? (unsigned short)best : 0xffff;
+                }
+                const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
+                if (px < S && py < S) fimb[py * S + px] = id;
+            }
+        }
+    } else {
+        // static blocks: wave w walks its NSUB blocks; the per-pixel state stays in registers over
+        // the staging rounds
+        float xp[NSUB], yp[NSUB];
+        float depth_min[NSUB];
+        int best[NSUB];
+        float xcl[NSUB], xch[NSUB], ycl[NSUB], ych[NSUB];
+#pragma unroll
+        for (int k = 0; k < NSUB; k++) {
+            int ox, oy;
+            C::block_of(wid, k, ox, oy);
+            xcl[k] = pix_center(bx0 + ox, S);
+            xch[k] = pix_center(bx0 + ox + 7, S);
+            ycl[k] = pix_center(by0 + oy, S);
+            ych[k] = pix_center(by0 + oy + 7, S);
+            xp[k] = pix_center(bx0 + ox + (lane & 7), S);
+            yp[k] = pix_center(by0 + oy + (lane >> 3), S);
+            depth_min[k] = far;
+            best[k] = -1;
+        }
+        uint32_t bits = bits0;
+        int total = total0, off = off0;
+        for (int wbase = 0;;) {
+            const int w = wbase + t;
+            ncand += total;
+            for (int cbase = 0; cbase < total; cbase += CAND) {
+                // expand my word's set bits into the ordered candidate list
+                int r = off;
+                for (uint32_t m = bits; m; m &= m - 1, r++) {
+                    if (r < cbase) continue;
+                    if (r >= cbase + CAND) break;
+                    s_cand[r - cbase] = w * 32 + __builtin_ctz(m);
                 }
                 __syncthreads();
+                const int nc = min(CAND, total - cbase);
+                for (int j0 = 0; j0 < nc; j0 += FCAP) {
+                    const int n = min(FCAP, nc - j0);
 #ifdef NR_FWD_TIMING
-                t_stage += clock64() - ts0_;  // staging rounds (the expansion is in the walk's share)
+                    const unsigned long long ts0_ = clock64();
+#endif
+                    if (t < n) {
+                        const int f = s_cand[j0 + t];
+                        stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
+                    }
+                    __syncthreads();
+#ifdef NR_FWD_TIMING
+                    t_stage += clock64() - ts0_;  // staging rounds (the expansion is in the walk's share)
 #endif
 #pragma unroll
-                for (int k = 0; k < NSUB; k++) {
-                    const float xc0 = xcl[k], xc1 = xch[k], yc0 = ycl[k], yc1 = ych[k];
-#if NR_FWD_DEFER
-                    int pend = -1;                // staging slot of my pixel's pending face
-                    unsigned long long occ = 0;   // the wave's pixels with a pending face
-#endif
-                    for (int c0 = 0; c0 < n; c0 += 64) {
-                        bool hit = false;
-                        if (c0 + lane < n) {
-                            const float4 q0 = s_face[c0 + lane];
-                            hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
-                            if (CULL && hit)
-                                hit = !block_culled<FCAP>(s_face + c0 + lane, 0.5f * (xc0 + xc1), 0.5f * (yc0 + yc1),
-                                                          0.5f * (xc1 - xc0), 0.5f * (yc1 - yc0));
-                        }
-                        // faces touching this wave's pixels, walked in ascending order
-                        for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
-                            const int slot = c0 + __builtin_ctzll(m);
-                            const float4* e = s_face + slot;
-                            FaceRows<FCAP> fr;
-                            fr.load(e);
-#if NR_FWD_DEFER
-                            const bool pass = face_pass<FCAP>(e, fr, xp[k], yp[k], depth_min[k]);
-                            const unsigned long long cov = __ballot(pass);
-                            if (cov & occ) {  // commit first where this face would queue behind a pending one
-                                if (pend >= 0) face_commit<FCAP>(s_face + pend, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
-                                pend = -1;
-                                occ = 0;
-                            }
-                            if (pass) pend = slot;
-                            occ |= cov;
-#else
-                            face_test<FCAP>(e, fr, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
-#endif
-                        }
-                    }
-#if NR_FWD_DEFER
-                    if (pend >= 0) face_commit<FCAP>(s_face + pend, xp[k], yp[k], near, far, delta, depth_min[k], best[k]);
-#endif
+                    for (int k = 0; k < NSUB; k++)
+                        walk_block<FCAP, CULL, false>(s_face, n, lane, xp[k], yp[k], xcl[k], xch[k], ycl[k], ych[k], near,
+                                                      far, delta, depth_min[k], best[k]);
+                    __syncthreads();
                 }
-                __syncthreads();
+            }
+            wbase += NTF;
+            if (wbase >= g.nwords) break;
+            bits = (wbase + t < g.nwords) ? words[wbase + t] : 0u;
+            off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
+        }
+#pragma unroll
+        for (int k = 0; k < NSUB; k++) {
+            int ox, oy;
+            C::block_of(wid, k, ox, oy);
+            const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
+            if (px < S && py < S) fimb[py * S + px] = best[k];
+        }
+        if (SHADE && ncand > 0) {
+            // the bin's 32x32 face ids go through LDS (the staging area is free once every wave has walked)
+            int* s_fim = reinterpret_cast<int*>(s_raw);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < NSUB; k++) {
+                int ox, oy;
+                C::block_of(wid, k, ox, oy);
+                s_fim[(oy + (lane >> 3)) * COARSE + ox + (lane & 7)] = best[k];
             }
         }
     }
 
     NR_FTSTAMP(3, clock64());
     NR_FTSTAMP(2, t_stage);
-#pragma unroll
-    for (int k = 0; k < NSUB; k++) {
-        int ox, oy;
-        C::block_of(wid, k, ox, oy);
-        const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
-        if (px < S && py < S) fimb[py * S + px] = best[k];
-    }
     // may the bin hold a foreground pixel (the backward skips its tiles when not): a bin without
     // candidate faces holds none
     if (binfg && t == 0) binfg[(long long)b * g.nbins + bin] = ncand > 0 ? 1 : 0;
@@ -613,30 +702,38 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
         if (iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, halo);
+        NR_FTSTAMP(4, clock64());
+        NR_FTSTAMP(5, clock64());
+        NR_FTSTAMP(6, 0ull);
         return;
     }
     if (SHADE) {
-        // the bin's 32x32 face ids go through LDS (the staging area is free once every wave has
-        // walked); thread t then shades the output pixel whose internal quad is (2 (t >> 4), 2 (t & 15))
+        // thread t shades the output pixel whose internal quad is (2 (t >> 4), 2 (t & 15)), from the
+        // face ids in LDS (dyn: the winners' staging slots)
         Shade sh = sh_in;
         sh.nl = 0;
         sh.bg = nullptr;
-        int* s_fim = reinterpret_cast<int*>(s_raw);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < NSUB; k++) {
-            int ox, oy;
-            C::block_of(wid, k, ox, oy);
-            s_fim[(oy + (lane >> 3)) * COARSE + ox + (lane & 7)] = best[k];
-        }
         __syncthreads();
         NR_FTSTAMP(4, clock64());
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
         if (iy + 1 < S && ix + 1 < S) {
-            const int2 q0 = *reinterpret_cast<const int2*>(s_fim + (2 * m) * COARSE + 2 * n);      // d, b
-            const int2 q1 = *reinterpret_cast<const int2*>(s_fim + (2 * m + 1) * COARSE + 2 * n);  // c, a
-            const int fis[4] = {q1.y, q0.y, q1.x, q0.x};
+            int fis[4];
+            if (dyn) {
+                const uint32_t q0 = *reinterpret_cast<const uint32_t*>(s_slot + (2 * m) * COARSE + 2 * n);      // d, b
+                const uint32_t q1 = *reinterpret_cast<const uint32_t*>(s_slot + (2 * m + 1) * COARSE + 2 * n);  // c, a
+                const uint32_t sl[4] = {q1 >> 16, q0 >> 16, q1 & 0xffff, q0 & 0xffff};
+#pragma unroll
+                for (int i = 0; i < 4; i++) fis[i] = sl[i] == 0xffff ? -1 : __float_as_int(s_face[FCAP + sl[i]].w);
+            } else {
+                const int* s_fim = reinterpret_cast<const int*>(s_raw);
+                const int2 q0 = *reinterpret_cast<const int2*>(s_fim + (2 * m) * COARSE + 2 * n);      // d, b
+                const int2 q1 = *reinterpret_cast<const int2*>(s_fim + (2 * m + 1) * COARSE + 2 * n);  // c, a
+                fis[0] = q1.y;
+                fis[1] = q0.y;
+                fis[2] = q1.x;
+                fis[3] = q0.x;
+            }
             shade_quad(sh, face_records + (long long)b * F * FACE_REC, b, S, iy, ix, fis, images, halo);
         }
         NR_FTSTAMP(5, clock64());

@@ -407,36 +407,14 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
 }
 
 // Edge cull of a staged face against an 8x8 block (NR_FWD_CULL, deep-bin variant): true only when
-// the reference's edge tests (.cu:107-116) fail at every pixel centre of the block. Edge k's
-// function c_k is affine in the pixel, so its range over the block is centre +- half-range; a sign
-// is trusted when the whole range clears a margin covering the rounding of the reference's own float
-// evaluation and of this one (2^-18 of the magnitude bound T, at least 2^-60 so that a product of
-// two trusted values cannot underflow to 0). The tests fail at a pixel when c1 c2 < 0 or c2 c3 < 0,
-// so the block is culled when c1, c2 or c2, c3 have trusted opposite signs, or c1, c3 do and c2 has
-// a trusted sign (with c2 exactly 0 the reference passes the pixel whatever c1 and c3 are). NaN and
-// infinite operands never produce a trusted sign.
+// the reference's edge tests (.cu:107-116) fail at every pixel centre of the block (nr_cull.h)
 #ifndef NR_FWD_CULL
 #define NR_FWD_CULL 1
 #endif
-__device__ __forceinline__ void edge_sign(float ax, float ay, float A, float B, float xc, float yc, float hx, float hy,
-                                          bool& pos, bool& neg) {
-    const float dy = yc - ay, dx = xc - ax;
-    const float cc = dy * A - B * dx;
-    const float aA = fabsf(A), aB = fabsf(B);
-    const float hr = hy * aA + hx * aB;
-    const float T = (fabsf(yc) + fabsf(ay) + hy) * aA + (fabsf(xc) + fabsf(ax) + hx) * aB;
-    const float m = fmaxf(T * 0x1p-18f, 0x1p-60f) + hr;
-    pos = cc > m;
-    neg = cc < -m;
-}
 template <int FST>
 __device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc, float hx, float hy) {
     const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
-    bool p1, n1, p2, n2, p3, n3;
-    edge_sign(q2.x, q2.y, q4.y, q4.z, xc, yc, hx, hy, p1, n1);  // c1: (x0, y0), A = x1 - x0, B = y1 - y0
-    edge_sign(q2.z, q2.w, q4.w, q5.x, xc, yc, hx, hy, p2, n2);  // c2: (x1, y1), C, D
-    edge_sign(q3.x, q3.y, q5.y, q5.z, xc, yc, hx, hy, p3, n3);  // c3: (x2, y2), E, F
-    return (p1 && n2) || (n1 && p2) || (p2 && n3) || (n2 && p3) || (((p1 && n3) || (n1 && p3)) && (p2 || n2));
+    return nr_block_culled(q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q4.y, q4.z, q4.w, q5.x, q5.y, q5.z, xc, yc, hx, hy);
 }
 
 // one wave's walk of the n staged faces over its 8x8 block (pixel (xp, yp) per lane, pixel-centre
@@ -538,7 +516,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
                                                   int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
                                                   float* __restrict__ halo, uint8_t* __restrict__ binfg) {
     using C = FwdCfg<NTF>;
-    static_assert(!SHADE || (NTF == 256 && COARSE == 32), "fused shading: one output pixel per thread");
+    static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
     constexpr bool CULL = NR_FWD_CULL && NTF >= 512;  // deep bins: small faces over each 8x8 block
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
@@ -719,7 +697,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         Shade sh = sh_in;
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
-        if (iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, halo);
+        if ((NTF == 256 || t < 256) && iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, halo);
         NR_FTSTAMP(4, clock64());
         NR_FTSTAMP(5, clock64());
         NR_FTSTAMP(6, 0ull);
@@ -735,7 +713,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         NR_FTSTAMP(4, clock64());
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
-        if (iy + 1 < S && ix + 1 < S) {
+        if ((NTF == 256 || t < 256) && iy + 1 < S && ix + 1 < S) {
             int fis[4];
             if (dyn) {
                 const uint32_t q0 = *reinterpret_cast<const uint32_t*>(s_slot + (2 * m) * COARSE + 2 * n);      // d, b

@@ -45,9 +45,13 @@
 #ifndef NR_FUSE_SHADE
 #define NR_FUSE_SHADE 1  // 0: k_shade always has its own launch (timing builds)
 #endif
+#ifndef NR_FUSE_SHADE1024
+#define NR_FUSE_SHADE1024 1  // the deep-bin / small-grid 1024-thread variant shades too (threads 0-255)
+#endif
 
 #pragma clang fp contract(off)
 
+#include "nr_cull.h"
 #include "nr_common.h"
 #include "nr_shade.h"
 #include "nr_fwd.h"
@@ -136,7 +140,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     const double faces_per_bin = (double)F / g.nbins;
     const int ntf = NR_FWD_FORCE_NT ? NR_FWD_FORCE_NT : ((blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024);
     const Shade sh = ra ? make_shade(ra) : Shade{};
-    const bool fuse = NR_FUSE_SHADE && ra && ntf == 256 && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
+    const bool fuse = NR_FUSE_SHADE && ra && (ntf == 256 || (NR_FUSE_SHADE1024 && ntf == 1024)) && ra->anti_aliasing &&
+                      sh.nl == 0 && !sh.bg && vertices;
     // per-bin foreground flags after the halo values (the backward skips background tiles)
     uint8_t* binfg = (ra && ra->halo) ? (uint8_t*)ra->halo + halo_flags_offset_bytes(B, S, sh.C) : nullptr;
     {
@@ -145,7 +150,10 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         // over and the bins are shallow; 1024 when it does not, or when the bins are deep (F per bin
         // at the 32x32 bin granularity as the depth proxy)
         const int rs = vertices ? FACE_REC : 9;
-        if (fuse)
+        if (fuse && ntf == 1024)
+            hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
+        else if (fuse)
             hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
                                F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
         else if (ntf == 256)

@@ -155,3 +155,19 @@ def test_make_gif(tmp_path):
     g = Image.open(out)
     assert g.n_frames == 3
     assert not list(tmp_path.glob('_tmp_*.png'))
+
+
+def test_edge_cull_is_exact_on_host(tmp_path):
+    """The forward's edge cull (csrc/nr_cull.h, the same header the kernel includes) compiled for
+    the host: over random, pixel-snapped (c2 exactly 0 along an axis-aligned edge 1-2), tiny,
+    degenerate and non-finite triangles, no culled 8x8 block has a pixel centre that passes the
+    reference's edge tests (.cu:107-116) -- the face would have been walked for nothing, never
+    missed. The check also culls about half the cases, so it is not vacuous."""
+    import subprocess
+    exe = str(tmp_path / "cull_check")
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-I" + os.path.join(ROOT, "neural_renderer_v2_pytorch_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "host", "cull_check.cpp"), "-o", exe])
+    out = subprocess.run([exe, "2000000"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    m = re.match(r"checked (\d+) culled (\d+) passes-in-culled (\d+)", out.stdout)
+    assert m and int(m.group(3)) == 0 and int(m.group(2)) > int(m.group(1)) // 4, out.stdout

@@ -145,6 +145,13 @@ typedef struct NrRasterArgs {
      * backward then sample (one 16-B load per bilinear corner); kept by the caller from the forward
      * to the backward.  NULL = sample `textures` directly (same results). */
     float* textures_packed;
+    /* optional: the backward's workspace (nr_backward_workspace_bytes), allocated before the forward.
+     * The forward zeroes its first bwd_workspace_bytes bytes (the backward's accumulators) from the
+     * face-setup launch, and nr_rasterize_backward called with this same pointer as its workspace
+     * skips its own zero fill. Name it in one backward only: after a backward its accumulators are
+     * no longer zero. NULL = the backward zero-fills its workspace. */
+    void* bwd_workspace;
+    size_t bwd_workspace_bytes;
 } NrRasterArgs;
 
 enum { NR_LIGHT_AMBIENT = 0, NR_LIGHT_DIRECTIONAL = 1, NR_LIGHT_SPECULAR = 2, NR_LIGHT_FLOATS = 8 };

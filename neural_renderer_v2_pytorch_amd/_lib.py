@@ -47,6 +47,7 @@ class NrRasterArgs(ctypes.Structure):
         ("normal_offsets", c_void_p), ("normal_faces", c_void_p),
         ("backgrounds", c_void_p), ("bg_stride_b", c_ll), ("bg_stride_c", c_ll), ("bg_stride_y", c_ll),
         ("grad_backgrounds", c_void_p), ("textures_packed", c_void_p),
+        ("bwd_workspace", c_void_p), ("bwd_workspace_bytes", c_size_t),
     ]
 
 NR_LIGHT_AMBIENT, NR_LIGHT_DIRECTIONAL, NR_LIGHT_SPECULAR, NR_LIGHT_FLOATS = 0, 1, 2, 8

@@ -686,6 +686,12 @@ __device__ __forceinline__ void tex_out_one(const TexOut& to, long long i) {
     to.out[(bt * 3 + 2) * to.HW + p] = v.z + pl[2 * to.HW];
 }
 // this block's slice [lo, hi) of n items spread over the whole grid
+// the backward's accumulators, zeroed by the forward's face setup (NrRasterArgs.bwd_workspace)
+struct ZeroFill {
+    float4* __restrict__ p;  // null: nothing to zero
+    long long n16;           // 16-byte units
+};
+
 __device__ __forceinline__ void grid_slice(long long n, long long& lo, long long& hi) {
     const long long nb = (long long)gridDim.x * gridDim.y;
     const long long id = (long long)blockIdx.y * gridDim.x + blockIdx.x;

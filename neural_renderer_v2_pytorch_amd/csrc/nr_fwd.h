@@ -18,7 +18,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     uint32_t* __restrict__ mask, int nbx, int nbins, int nwords,
                                                     const float* __restrict__ vt, long long vt_bstride, int Vt,
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
-                                                    int uv_items, float* __restrict__ fnorm, TexPack pk) {
+                                                    int uv_items, float* __restrict__ fnorm, TexPack pk, ZeroFill zf) {
     __shared__ int2 s_bb[SETUP_FACES];
     // the block's face records, assembled per face and then written out coalesced (a record per lane
     // would store 64-B strided rows); the bin-mask words reuse the space afterwards
@@ -32,6 +32,11 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         long long lo, hi;
         grid_slice(pk.n, lo, hi);
         for (long long i = lo + (t - SETUP_FACES); i < hi; i += blockDim.x - SETUP_FACES) tex_pack_one(pk, i);
+    }
+    if (zf.p && t >= SETUP_FACES) {  // and zero the backward's accumulators (NrRasterArgs.bwd_workspace)
+        long long lo, hi;
+        grid_slice(zf.n16, lo, hi);
+        for (long long i = lo + (t - SETUP_FACES); i < hi; i += blockDim.x - SETUP_FACES) zf.p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (t < SETUP_FACES) {
         const int f = f0 + t;

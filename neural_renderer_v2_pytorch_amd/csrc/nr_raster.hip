@@ -91,7 +91,7 @@ size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
 static int run_face_index(const float* vertices, const int32_t* faces_idx, float* face_records, int32_t* fim,
                           int B, int V, int F, int S, float near, float far, int draw_backside, float delta,
                           void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images,
-                          TexPack pk) {
+                          TexPack pk, ZeroFill zf = ZeroFill{nullptr, 0}) {
     Geom g = make_geom(F, S);
     g.group = group_for(B, NR_FWD_GROUP);
     int2* bbox = (int2*)ws;
@@ -107,6 +107,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         if (e) return e;
         pk.out = nullptr;
     }
+    if (F == 0 && zf.p && hipMemsetAsync(zf.p, 0, (size_t)zf.n16 * 16, st) != hipSuccess)
+        return check_launch("hipMemsetAsync");
     if (F > 0) {
         dim3 grid((F + SETUP_FACES - 1) / SETUP_FACES, B);
         const bool rgb = ra && (ra->draw_flags & NR_DRAW_RGB);
@@ -119,11 +121,11 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
-                               rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk);
+                               rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk, zf);
         else
             hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
-                               nullptr, pk);
+                               nullptr, pk, zf);
         int e = check_launch("k_face_setup");
         if (e) return e;
         if (lit && V > 0) {
@@ -257,10 +259,18 @@ int nr_rasterize_forward(const NrRasterArgs* a, float* images, void* stream) {
         pk.out = reinterpret_cast<float4*>(a->textures_packed);
         pk.n = (long long)tex_items * pk.HWp;
     }
+    // the backward's accumulators, zeroed by the setup's idle threads (no memset launch in the backward)
+    ZeroFill zf{nullptr, 0};
+    if (a->bwd_workspace && a->bwd_workspace_bytes > 0) {
+        if (((uintptr_t)a->bwd_workspace & 15) || (a->bwd_workspace_bytes & 15))
+            return fail(NR_ERR_ARGS, "bwd_workspace must be 16-byte aligned and sized");
+        zf.p = reinterpret_cast<float4*>(a->bwd_workspace);
+        zf.n16 = (long long)(a->bwd_workspace_bytes / 16);
+    }
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
     return run_face_index(a->vertices, a->faces, a->face_records, a->face_index, a->batch_size, a->num_vertices,
                           a->num_faces, S, a->near, a->far, a->draw_backside, a->depth_min_delta, a->workspace,
-                          a->workspace_bytes, (hipStream_t)stream, a, images, pk);
+                          a->workspace_bytes, (hipStream_t)stream, a, images, pk, zf);
 }
 
 size_t nr_texture_packed_bytes(int texture_items, int tex_height, int tex_width) {
@@ -277,7 +287,8 @@ size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw
 }
 
 // backward workspace: [gF: B F 9 face-corner floats][g4: Bt HWp RGBA texel rows][planar: Bt 3 H W]
-// [lights: gN: B F 9][gU: B V 3]; everything before gU starts at zero (one memset)
+// [lights: gN: B F 9][gU: B V 3]; everything before gU starts at zero (one memset, or the forward's
+// setup zeroed it: NrRasterArgs.bwd_workspace)
 size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num_vertices, int texture_items,
                                    int tex_height, int tex_width, int num_lights) {
     const size_t hw = (size_t)tex_height * tex_width, hwp = (hw + 3) & ~size_t(3);
@@ -328,7 +339,10 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     float* gU = lit ? (float*)(w + align_up((size_t)a->batch_size * a->num_faces * 9 * 4)) : nullptr;
     // gU is fully written by k_vnormal_bwd; the accumulators before it start at zero
     const size_t zero_bytes = lit ? (size_t)((char*)gU - (char*)workspace) : need;
-    if (zero_bytes > 0 && hipMemsetAsync(workspace, 0, zero_bytes, st) != hipSuccess) return check_launch("hipMemsetAsync");
+    // ... unless the forward zeroed them (NrRasterArgs.bwd_workspace names this workspace)
+    const bool prezeroed = a->bwd_workspace && a->bwd_workspace == workspace && a->bwd_workspace_bytes >= zero_bytes;
+    if (zero_bytes > 0 && !prezeroed && hipMemsetAsync(workspace, 0, zero_bytes, st) != hipSuccess)
+        return check_launch("hipMemsetAsync");
     BwdArgs ba;
     ba.face_records = a->face_records;
     ba.fim = a->face_index;

@@ -283,6 +283,9 @@ _HALO_CACHE = os.environ.get("NR_HALO_CACHE", "1") != "0"
 # the forward packs the texels into RGBA rows that forward and backward sample (NrRasterArgs.
 # textures_packed); False samples the [B, 3, H, W] textures directly (same results)
 _TEX_PACK = os.environ.get("NR_TEX_PACK", "1") != "0"
+# True: the forward allocates the backward's workspace and its setup launch zeroes the accumulators
+# (NrRasterArgs.bwd_workspace); False: the backward allocates and zero-fills it (same results)
+_BWD_PREZERO = os.environ.get("NR_BWD_PREZERO", "1") != "0"
 _TEX_PACK_MAX_BYTES = 1 << 31
 
 
@@ -338,8 +341,19 @@ class Rasterize(torch.autograd.Function):
                 tex4 = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
         a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws,
                   halo=halo, light=light, bg=bg, tex4=tex4)
+        # the backward's workspace, allocated now so that the forward's setup launch zeroes its
+        # accumulators (NrRasterArgs.bwd_workspace): the backward then has no zero fill of its own
+        bws = None
+        if _BWD_PREZERO and any(ctx.needs_input_grad[:2]):
+            H, W = cfg.tex_hw
+            tex_items = (1 if cfg.tex_shared else B) if (rgb and ctx.needs_input_grad[1]) else 0
+            nl = light_recs.shape[0] if light_recs is not None else 0
+            bws = torch.empty(L.nr_backward_workspace_bytes(B, cfg.F, cfg.V, tex_items, H, W, nl), dtype=torch.uint8,
+                              device=dev)
+            a.bwd_workspace, a.bwd_workspace_bytes = bws.data_ptr(), bws.numel()
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_forward(a, _lib.ptr(images), _lib.stream_of(vertices)), "nr_rasterize_forward")
+        ctx.bws = bws  # zeroed for the first backward only (its accumulators are spent after it)
         ctx.cfg = cfg
         ctx.light = light
         ctx.tex4 = tex4
@@ -378,8 +392,10 @@ class Rasterize(torch.autograd.Function):
             gt = torch.empty((tex_items, 3, H, W), dtype=torch.float32, device=dev)
         H, W = cfg.tex_hw
         nl = ctx.light[0].shape[0] if ctx.light is not None else 0
-        ws = torch.empty(L.nr_backward_workspace_bytes(cfg.B, cfg.F, cfg.V, tex_items, H, W, nl), dtype=torch.uint8,
-                         device=dev)
+        need = L.nr_backward_workspace_bytes(cfg.B, cfg.F, cfg.V, tex_items, H, W, nl)
+        prezeroed = ctx.bws is not None and ctx.bws.numel() == need
+        ws = ctx.bws if prezeroed else torch.empty(need, dtype=torch.uint8, device=dev)
+        ctx.bws = None
         adj = _vertex_adjacency(faces, cfg.V)
         gbg = None
         if backgrounds is not None and ctx.needs_input_grad[5]:
@@ -387,6 +403,8 @@ class Rasterize(torch.autograd.Function):
         bg = (backgrounds, gbg) if backgrounds is not None else None
         a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo, ctx.light, bg,
                   tex4=ctx.tex4)
+        if prezeroed:  # the forward zeroed it: no fill in the backward
+            a.bwd_workspace, a.bwd_workspace_bytes = ws.data_ptr(), ws.numel()
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),
                                                ws.numel(), _lib.stream_of(vertices)), "nr_rasterize_backward")

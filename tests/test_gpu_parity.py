@@ -926,3 +926,34 @@ def test_hip_graph_capture_matches_eager(dev):
     assert torch.equal(img, eager)
     close_grads(pv.grad, eager_gv, "graph grad vertices")
     close_grads(tx.grad, eager_gt, "graph grad textures")
+
+
+@pytest.mark.gpu
+def test_backward_workspace_zeroed_by_forward(dev):
+    """The forward's setup zeroes the backward's accumulators (NrRasterArgs.bwd_workspace): the
+    gradients match a backward that zero-fills its own workspace, and a second backward through the
+    same graph (retain_graph; the workspace is no longer zero) still adds the same gradients."""
+    B = 3
+    proj, f = _ico_batch(3, B, dev)
+    faces = torch.as_tensor(f, device=dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.as_tensor(np.random.RandomState(5).uniform(0, 1, tex.shape).astype(np.float32), device=dev)
+    g = torch.as_tensor(np.random.RandomState(6).normal(size=(B, 5, 64, 64)).astype(np.float32), device=dev)
+    out = {}
+    for prezero in (False, True):
+        nrr._BWD_PREZERO = prezero
+        try:
+            v = proj.detach().to(dev).requires_grad_(True)
+            t = tex.detach().clone().requires_grad_(True)
+            params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                                       faces_textures=torch.as_tensor(ft, device=dev), textures=t[None].expand(B, -1, -1, -1))
+            img = nrr.rasterize_core(v, faces, params, nr.RasterizeHyperparam(image_size=64))
+            img.backward(g, retain_graph=True)
+            g1 = (v.grad.clone(), t.grad.clone())
+            img.backward(g)
+            out[prezero] = (g1, (v.grad.clone(), t.grad.clone()))
+        finally:
+            nrr._BWD_PREZERO = True
+    for i in range(2):
+        torch.testing.assert_close(out[True][0][i], out[False][0][i], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(out[True][1][i], 2 * out[True][0][i], rtol=1e-5, atol=1e-6)

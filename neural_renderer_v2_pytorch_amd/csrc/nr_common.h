@@ -700,4 +700,13 @@ __device__ __forceinline__ void grid_slice(long long n, long long& lo, long long
     hi = min(lo + chunk, n);
 }
 
+// this block's slice of the zero fill, by all its threads, as its last work (the stores would
+// otherwise count in the vmcnt waits of the block's loads)
+__device__ __forceinline__ void zero_fill(const ZeroFill& zf) {
+    if (!zf.p) return;
+    long long lo, hi;
+    grid_slice(zf.n16, lo, hi);
+    for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) zf.p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 }  // namespace

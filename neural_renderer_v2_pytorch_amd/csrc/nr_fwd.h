@@ -33,11 +33,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         grid_slice(pk.n, lo, hi);
         for (long long i = lo + (t - SETUP_FACES); i < hi; i += blockDim.x - SETUP_FACES) tex_pack_one(pk, i);
     }
-    if (zf.p && t >= SETUP_FACES) {  // and zero the backward's accumulators (NrRasterArgs.bwd_workspace)
-        long long lo, hi;
-        grid_slice(zf.n16, lo, hi);
-        for (long long i = lo + (t - SETUP_FACES); i < hi; i += blockDim.x - SETUP_FACES) zf.p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+
     if (t < SETUP_FACES) {
         const int f = f0 + t;
         int2 bb = make_int2(NR_EMPTY_RANGE, NR_EMPTY_RANGE);
@@ -152,6 +148,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
             const int bin = p / nw, wi = p % nw;
             mask[((long long)b * nbins + bin) * nwords + w0 + wi] = s_mask[bin * (SETUP_FACES / 32) + wi];
         }
+        zero_fill(zf);
         return;
     }
     for (int p = t; p < nbins * nw; p += blockDim.x) {
@@ -168,6 +165,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         }
         mask[((long long)b * nbins + bin) * nwords + w0 + wi] = bits;
     }
+    zero_fill(zf);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -286,6 +286,10 @@ _TEX_PACK = os.environ.get("NR_TEX_PACK", "1") != "0"
 # True: the forward allocates the backward's workspace and its setup launch zeroes the accumulators
 # (NrRasterArgs.bwd_workspace); False: the backward allocates and zero-fills it (same results)
 _BWD_PREZERO = os.environ.get("NR_BWD_PREZERO", "1") != "0"
+# only small workspaces: there the separate zero fill is a latency-bound launch (headline: 12 MB,
+# step 0.516 -> 0.505 ms); a large one is bandwidth-bound either way and only lengthens the setup
+# (the car with its atlas gradient: 63 MB, setup 0.052 -> 0.063 ms, step no better)
+_BWD_PREZERO_MAX = 32 << 20
 _TEX_PACK_MAX_BYTES = 1 << 31
 
 
@@ -348,9 +352,10 @@ class Rasterize(torch.autograd.Function):
             H, W = cfg.tex_hw
             tex_items = (1 if cfg.tex_shared else B) if (rgb and ctx.needs_input_grad[1]) else 0
             nl = light_recs.shape[0] if light_recs is not None else 0
-            bws = torch.empty(L.nr_backward_workspace_bytes(B, cfg.F, cfg.V, tex_items, H, W, nl), dtype=torch.uint8,
-                              device=dev)
-            a.bwd_workspace, a.bwd_workspace_bytes = bws.data_ptr(), bws.numel()
+            nbytes = L.nr_backward_workspace_bytes(B, cfg.F, cfg.V, tex_items, H, W, nl)
+            if nbytes <= _BWD_PREZERO_MAX:
+                bws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                a.bwd_workspace, a.bwd_workspace_bytes = bws.data_ptr(), bws.numel()
         with torch.cuda.device(dev):
             _lib.check(L.nr_rasterize_forward(a, _lib.ptr(images), _lib.stream_of(vertices)), "nr_rasterize_forward")
         ctx.bws = bws  # zeroed for the first backward only (its accumulators are spent after it)

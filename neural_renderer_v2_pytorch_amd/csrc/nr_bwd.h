@@ -169,6 +169,9 @@ __device__ __forceinline__ float chunk_reduce_scatter(float v0, float v1, float 
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);           // row c: v_c
 }
 
+#ifdef NR_COUNT_DIRECT
+__device__ unsigned long long g_ncount[4];  // debug builds: windowed / direct samples, direct without a window
+#endif
 // per interior pixel state carried across the stencil's barrier
 struct BwdPix {
     int fi;            // face index (-1: background or outside)
@@ -399,6 +402,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                     fits = fits && cx >= 0 && cx < TWIN && cy >= 0 && cy < TWIN && gx_ >= 0 && gy_ >= 0 &&
                            gx_ < sh.tv.W && gy_ < sh.tv.H;
                 }
+#ifdef NR_COUNT_DIRECT
+                atomicAdd(&g_ncount[fits ? 0 : 1], 1ull);
+                if (!fits && !wok) atomicAdd(&g_ncount[2], 1ull);
+#endif
                 if (fits) {
                     q.pos = dx + 4 * dy;  // window texel of the top-left corner (dx, dy in 0..2)
                 } else {

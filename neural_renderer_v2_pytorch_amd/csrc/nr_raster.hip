@@ -539,6 +539,13 @@ __attribute__((visibility("default"))) int nr_debug_fwd_timing(unsigned long lon
     return NR_OK;
 }
 #endif
+#ifdef NR_COUNT_DIRECT
+__attribute__((visibility("default"))) int nr_debug_counts(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ncount), 4 * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(NR_ERR_LAUNCH, "hipMemcpyFromSymbol failed");
+    return NR_OK;
+}
+#endif
 #ifdef NR_BWD_TIMING
 // timing builds only: the backward's per-wave phase timestamps (g_bwd_t), n entries to host memory
 __attribute__((visibility("default"))) int nr_debug_bwd_timing(unsigned long long* out, size_t n) {

@@ -405,6 +405,16 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 #ifdef NR_COUNT_DIRECT
                 atomicAdd(&g_ncount[fits ? 0 : 1], 1ull);
                 if (!fits && !wok) atomicAdd(&g_ncount[2], 1ull);
+                {  // direct samples whose top-left texel a lower lane of the wave also samples directly
+                    const unsigned long long dm = __ballot(!fits);
+                    bool dup = false;
+                    for (unsigned long long m = dm; m; m &= m - 1) {
+                        const int j = __builtin_ctzll(m);
+                        const int oj = __builtin_amdgcn_readlane(s.idx[0], j);
+                        dup = dup || (j < (int)(threadIdx.x & 63) && oj == s.idx[0]);
+                    }
+                    if (!fits && dup) atomicAdd(&g_ncount[3], 1ull);
+                }
 #endif
                 if (fits) {
                     q.pos = dx + 4 * dy;  // window texel of the top-left corner (dx, dy in 0..2)

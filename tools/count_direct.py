@@ -16,4 +16,5 @@ L = _lib.lib()
 step(); torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 4)()
 L.nr_debug_counts(buf)
-print("after 1 step: windowed %d direct %d direct-without-window %d" % (buf[0], buf[1], buf[2]))
+print("after 1 step: windowed %d direct %d direct-without-window %d; direct whose top-left texel a lower lane of the "
+      "wave (same pixel row k) also samples directly: %d" % (buf[0], buf[1], buf[2], buf[3]))

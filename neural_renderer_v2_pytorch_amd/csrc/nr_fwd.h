@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                 u[0] = make_float4(uv[0], uv[1], uv[2], uv[3]);
                 u[1] = make_float4(uv[4], uv[5], __int_as_float(uok ? 1 : 0), 0.f);
             }
-            bbox[(long long)b * F + f] = bb;
+            (void)bbox;  // the pixel bbox stays in LDS (the masks); the forward stages float bounds itself
         }
         s_bb[t] = bb;
     }
@@ -211,16 +211,19 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //   (the bin's walks run 4x wider: small batches, where the grid is a few blocks per CU, and dense
 //   bins -- 300+ faces over one 8x8 block on a 50k-face torus -- no longer serialise on 4 waves).
 //   LDS face record, structure of arrays (float4 i of staged face j at s_face[i * FCAP + j]: the
-//   staging stores are lane-contiguous), 8 x float4:
-//     0: xmin xmax ymin ymax | 1: bx by zmin id | 2: x0 y0 x1 y1 | 3: x2 y2 z0 z1
-//     4: z2 A=x1-x0 B=y1-y0 C=x2-x1 | 5: D=y2-y1 E=x0-x2 F=y0-y2 k0 | 6: k1 k2 1/z0 1/z1 | 7: 1/z2 - - ok
+//   staging stores are lane-contiguous), 7 x float4; the pass test reads rows 0-4, the commit 1-6:
+//     0: xmin xmax ymin ymax | 1: zmin x0 y0 x1 | 2: y1 x2 y2 A=x1-x0 | 3: B=y1-y0 C=x2-x1 D=y2-y1 E=x0-x2
+//     4: F=y0-y2 k0 k1 k2 | 5: z0 z1 z2 id | 6: 1/z0 1/z1 1/z2 ok
 //   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
-constexpr int FREC = 8;  // float4 per staged face
+constexpr int FREC = 7;  // float4 per staged face
+#ifndef NR_FWD_FCAP256
+#define NR_FWD_FCAP256 128  // staged faces per round of the 256-thread variant (8 blocks per CU need <= 20 KB of LDS)
+#endif
 template <int NTF> struct FwdCfg {
     static constexpr int NW = NTF / 64;                        // waves
     static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
     static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
-    static constexpr int FCAP = NTF >= 512 ? 256 : 128;        // faces staged per round
+    static constexpr int FCAP = NTF >= 512 ? 256 : NR_FWD_FCAP256;  // faces staged per round
     static constexpr int LDS = FCAP * FREC * 16 + CAND * 4;
     static_assert(NSUB == 1 || NSUB == 2 || NSUB == 4, "forward block layout");
     // 8x8 block k of wave w: its origin (ox, oy) in the bin
@@ -243,11 +246,11 @@ template <int NTF> struct FwdCfg {
 // NR_FWD_EAGER: how many of the record's float4 rows the walk loads before the first test (2: the
 // tests load the rest as they go; 6: one LDS round trip for the depth, box and edge tests; 8: all)
 #ifndef NR_FWD_EAGER
-#define NR_FWD_EAGER 6  // measured: 2 -> 6 takes the headline forward 0.268 -> 0.259 ms, the car 1.20 -> 1.14 ms; 8 spills
+#define NR_FWD_EAGER 5  // the pass test's rows (8-row layout: 2 -> 6 eager rows took the headline forward 0.268 -> 0.259 ms, the car 1.20 -> 1.14 ms)
 #endif
 template <int FST>
 struct FaceRows {
-    float4 r[8];
+    float4 r[FREC];
     __device__ __forceinline__ void load(const float4* e) {
 #pragma unroll
         for (int i = 0; i < NR_FWD_EAGER; i++) r[i] = e[i * FST];
@@ -269,38 +272,38 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
     // The rejections of .cu:94-126 are independent of each other (none changes the state), so their
     // order is free: the depth-bound reject .cu:124-126 goes first, as it is the cheapest and lets a
     // whole wave skip a face hidden behind what its pixels already hold.
-    if (depth_min < q1.z) return;
+    if (depth_min < q1.x) return;
     // .cu:94-97 (min/max form, exact for non-NaN faces)
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
-    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4), q5 = fr.get(e, 5);
-    const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
+    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
+    const float x0 = q1.y, y0 = q1.z, x1 = q1.w, y1 = q2.x, x2 = q2.y, y2 = q2.z;
+    const float A = q2.w, B = q3.x, C = q3.y, D = q3.z, E = q3.w, F = q4.x;
     // .cu:107-116
-    const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
-    const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
+    const float c1 = (yp - y0) * A - B * (xp - x0);
+    const float c2 = (yp - y1) * C - D * (xp - x1);
     if (c1 * c2 < 0) return;
-    const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
+    const float c3 = (yp - y2) * E - F * (xp - x2);
     if (c2 * c3 < 0) return;
+    const float4 q5 = fr.get(e, 5), q6 = fr.get(e, 6);
 #if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 2
-    best = __float_as_int(q1.w);  // timing build: no division block
+    best = __float_as_int(q5.w);  // timing build: no division block
     return;
 #endif
-    const float4 q6 = fr.get(e, 6);
-    const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
+    const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
     // .cu:130-139
-    float w0 = (yp * q4.w - xp * q5.x) + q5.w;
-    float w1 = (yp * q5.y - xp * q5.z) + q6.x;
-    float w2 = (yp * q4.y - xp * q4.z) + q6.y;
+    float w0 = (yp * C - xp * D) + q4.y;
+    float w1 = (yp * E - xp * F) + q4.z;
+    float w2 = (yp * A - xp * B) + q4.w;
     const float ws = w0 + w1 + w2;
     float zp;
-    const float4 q7 = fr.get(e, 7);
-    if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
+    if (__float_as_int(q6.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
         // face coordinates and depths within [2^-20, 2^20] (or 0) bound every operand below inside
         // div_nr's exact range (DESIGN.md "Numerics"); 1/z is staged per face
         const float rs = rcp_nr(ws);
         w0 = div_nr(w0, ws, rs);
         w1 = div_nr(w1, ws, rs);
         w2 = div_nr(w2, ws, rs);
-        const float sum = div_nr(w0, z0, q6.z) + div_nr(w1, z1, q6.w) + div_nr(w2, z2, q7.x);
+        const float sum = div_nr(w0, z0, q6.x) + div_nr(w1, z1, q6.y) + div_nr(w2, z2, q6.z);
         if (in_range(sum, 0x1p-90f, 0x1p90f)) {
             const float r = rcp_nr(sum);
             zp = __builtin_fmaf(__builtin_fmaf(-sum, r, 1.f), r, r);  // div_nr(1, sum, r): 1 * r == r
@@ -317,7 +320,7 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
     if (zp <= near || far <= zp) return;
     if (zp <= depth_min - delta) {  // .cu:145-148
         depth_min = zp;
-        best = __float_as_int(q1.w);
+        best = __float_as_int(q5.w);
     }
 }
 
@@ -346,13 +349,13 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
 template <int FST>
 __device__ __forceinline__ bool face_pass(const float4* e, const FaceRows<FST>& fr, float xp, float yp, float depth_bound) {
     const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1);
-    if (depth_bound < q1.z) return false;
+    if (depth_bound < q1.x) return false;
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return false;
-    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4), q5 = fr.get(e, 5);
-    const float x0 = q2.x, y0 = q2.y, x1 = q2.z, y1 = q2.w, x2 = q3.x, y2 = q3.y;
-    const float c1 = (yp - y0) * q4.y - q4.z * (xp - x0);
-    const float c2 = (yp - y1) * q4.w - q5.x * (xp - x1);
-    const float c3 = (yp - y2) * q5.y - q5.z * (xp - x2);
+    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
+    const float x0 = q1.y, y0 = q1.z, x1 = q1.w, y1 = q2.x, x2 = q2.y, y2 = q2.z;
+    const float c1 = (yp - y0) * q2.w - q3.x * (xp - x0);  // A, B
+    const float c2 = (yp - y1) * q3.y - q3.z * (xp - x1);  // C, D
+    const float c3 = (yp - y2) * q3.w - q4.x * (xp - x2);  // E, F
 #if NR_FWD_PASS_BRANCHLESS
     return !(c1 * c2 < 0) && !(c2 * c3 < 0);
 #else
@@ -369,26 +372,27 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
     const float4 q1 = e[1 * FST];
 #if NR_FWD_COMMIT_EAGER
     // every row in one LDS round trip (the depth reject would otherwise wait for row 1 first)
-    const float4 q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST], q7 = e[7 * FST];
-    asm volatile("" ::"v"(q3.z), "v"(q3.w), "v"(q4.x), "v"(q4.y), "v"(q4.z), "v"(q4.w), "v"(q5.x), "v"(q5.y));
-    asm volatile("" ::"v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w), "v"(q7.x), "v"(q7.w));
-    if (depth_min < q1.z) return;
+    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
+    asm volatile("" ::"v"(q2.w), "v"(q3.x), "v"(q3.y), "v"(q3.z), "v"(q3.w), "v"(q4.x), "v"(q4.y), "v"(q4.z));
+    asm volatile("" ::"v"(q4.w), "v"(q5.x), "v"(q5.y), "v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w));
+    if (depth_min < q1.x) return;
 #else
-    if (depth_min < q1.z) return;
-    const float4 q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST], q7 = e[7 * FST];
+    if (depth_min < q1.x) return;
+    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
 #endif
-    const float z0 = q3.z, z1 = q3.w, z2 = q4.x;
-    float w0 = (yp * q4.w - xp * q5.x) + q5.w;
-    float w1 = (yp * q5.y - xp * q5.z) + q6.x;
-    float w2 = (yp * q4.y - xp * q4.z) + q6.y;
+    const float A = q2.w, B = q3.x, C = q3.y, D = q3.z, E = q3.w, F = q4.x;
+    const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
+    float w0 = (yp * C - xp * D) + q4.y;
+    float w1 = (yp * E - xp * F) + q4.z;
+    float w2 = (yp * A - xp * B) + q4.w;
     const float ws = w0 + w1 + w2;
     float zp;
-    if (__float_as_int(q7.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {  // as face_test
+    if (__float_as_int(q6.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {  // as face_test
         const float rs = rcp_nr(ws);
         w0 = div_nr(w0, ws, rs);
         w1 = div_nr(w1, ws, rs);
         w2 = div_nr(w2, ws, rs);
-        const float sum = div_nr(w0, z0, q6.z) + div_nr(w1, z1, q6.w) + div_nr(w2, z2, q7.x);
+        const float sum = div_nr(w0, z0, q6.x) + div_nr(w1, z1, q6.y) + div_nr(w2, z2, q6.z);
         if (in_range(sum, 0x1p-90f, 0x1p90f)) {
             const float r = rcp_nr(sum);
             zp = __builtin_fmaf(__builtin_fmaf(-sum, r, 1.f), r, r);
@@ -405,7 +409,7 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
     if (zp <= near || far <= zp) return;
     if (zp <= depth_min - delta) {
         depth_min = zp;
-        best = SLOT ? slot : __float_as_int(q1.w);
+        best = SLOT ? slot : __float_as_int(q5.w);
     }
 }
 
@@ -416,8 +420,8 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
 #endif
 template <int FST>
 __device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc, float hx, float hy) {
-    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST];
-    return nr_block_culled(q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q4.y, q4.z, q4.w, q5.x, q5.y, q5.z, xc, yc, hx, hy);
+    const float4 q1 = e[1 * FST], q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST];
+    return nr_block_culled(q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, q4.x, xc, yc, hx, hy);
 }
 
 // one wave's walk of the n staged faces over its 8x8 block (pixel (xp, yp) per lane, pixel-centre
@@ -467,21 +471,20 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
 }
 
 template <int FST>
-__device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f, int2 bb) {
+__device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f) {
     const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
     const float x2 = c[6], y2 = c[7], z2 = c[8];
     e[0 * FST] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
                        fmaxf(fmaxf(y0, y1), y2));
-    e[1 * FST] = make_float4(__int_as_float(bb.x), __int_as_float(bb.y), fminf(fminf(z0, z1), z2), __int_as_float(f));
-    e[2 * FST] = make_float4(x0, y0, x1, y1);
-    e[3 * FST] = make_float4(x2, y2, z0, z1);
-    e[4 * FST] = make_float4(z2, x1 - x0, y1 - y0, x2 - x1);
-    e[5 * FST] = make_float4(y2 - y1, x0 - x2, y0 - y2, x1 * y2 - x2 * y1);
-    e[6 * FST] = make_float4(x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, rcp_nr(z0), rcp_nr(z1));
+    e[1 * FST] = make_float4(fminf(fminf(z0, z1), z2), x0, y0, x1);
+    e[2 * FST] = make_float4(y1, x2, y2, x1 - x0);
+    e[3 * FST] = make_float4(y1 - y0, x2 - x1, y2 - y1, x0 - x2);
+    e[4 * FST] = make_float4(y0 - y2, x1 * y2 - x2 * y1, x2 * y0 - x0 * y2, x0 * y1 - x1 * y0);
+    e[5 * FST] = make_float4(z0, z1, z2, __int_as_float(f));
     const bool ok = coord_ok(x0) && coord_ok(y0) && coord_ok(x1) && coord_ok(y1) && coord_ok(x2) && coord_ok(y2) &&
                     in_range(z0, 0x1p-20f, 0x1p20f) && in_range(z1, 0x1p-20f, 0x1p20f) &&
                     in_range(z2, 0x1p-20f, 0x1p20f);
-    e[7 * FST] = make_float4(rcp_nr(z2), 0.f, 0.f, __int_as_float(ok ? 1 : 0));
+    e[6 * FST] = make_float4(rcp_nr(z0), rcp_nr(z1), rcp_nr(z2), __int_as_float(ok ? 1 : 0));
 }
 
 // per-wave phase timestamps of the fused forward (timing builds only, tools/fwd_timing.py)
@@ -538,7 +541,6 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: block extents in SGPRs
 
     const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
-    const int2* bbb = bbox + (long long)b * F;
     const float* frb = face_records + (long long)b * F * rs;
     int32_t* __restrict__ fimb = fim + (long long)b * S * S;
 
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
 #endif
             if (t < ncand) {
                 const int f = s_cand[t];
-                stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
+                stage_face<FCAP>(s_face + t, frb + f * rs, f);
             }
             __syncthreads();
 #ifdef NR_FWD_TIMING
@@ -596,8 +598,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
                                               pix_center(bx0 + ox + 7, S), pix_center(by0 + oy, S),
                                               pix_center(by0 + oy + 7, S), near, far, delta, depth_min, best);
                 int id = best;
-                if (SHADE) {  // best is the staging slot: its face id is in the record's row 1
-                    id = best >= 0 ? __float_as_int(s_face[FCAP + best].w) : -1;
+                if (SHADE) {  // best is the staging slot: its face id is in the record's row 5
+                    id = best >= 0 ? __float_as_int(s_face[5 * FCAP + best].w) : -1;
                     s_slot[(oy + (lane >> 3)) * COARSE + ox + (lane & 7)] = best >= 0 ? (unsigned short)best : 0xffff;
                 }
                 const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
@@ -646,7 +648,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
 #endif
                     if (t < n) {
                         const int f = s_cand[j0 + t];
-                        stage_face<FCAP>(s_face + t, frb + f * rs, f, bbb[f]);
+                        stage_face<FCAP>(s_face + t, frb + f * rs, f);
                     }
                     __syncthreads();
 #ifdef NR_FWD_TIMING
@@ -723,7 +725,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
                 const uint32_t q1 = *reinterpret_cast<const uint32_t*>(s_slot + (2 * m + 1) * COARSE + 2 * n);  // c, a
                 const uint32_t sl[4] = {q1 >> 16, q0 >> 16, q1 & 0xffff, q0 & 0xffff};
 #pragma unroll
-                for (int i = 0; i < 4; i++) fis[i] = sl[i] == 0xffff ? -1 : __float_as_int(s_face[FCAP + sl[i]].w);
+                for (int i = 0; i < 4; i++) fis[i] = sl[i] == 0xffff ? -1 : __float_as_int(s_face[5 * FCAP + sl[i]].w);
             } else {
                 const int* s_fim = reinterpret_cast<const int*>(s_raw);
                 const int2 q0 = *reinterpret_cast<const int2*>(s_fim + (2 * m) * COARSE + 2 * n);      // d, b

@@ -217,13 +217,16 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
 constexpr int FREC = 7;  // float4 per staged face
 #ifndef NR_FWD_FCAP256
-#define NR_FWD_FCAP256 128  // staged faces per round of the 256-thread variant (8 blocks per CU need <= 20 KB of LDS)
+#define NR_FWD_FCAP256 160  // staged faces per round of the 256-thread variant (8 blocks per CU need <= 20 KB of LDS; 128 -> 160: headline fwd 0.208 -> 0.195 ms)
+#endif
+#ifndef NR_FWD_FCAP1024
+#define NR_FWD_FCAP1024 512  // ... of the 1024-thread variant (2 blocks per CU: up to 80 KB each; 256 -> 512: car fwd 0.914 -> 0.81 ms, torus 0.151 -> 0.132 ms)
 #endif
 template <int NTF> struct FwdCfg {
     static constexpr int NW = NTF / 64;                        // waves
     static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
     static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
-    static constexpr int FCAP = NTF >= 512 ? 256 : NR_FWD_FCAP256;  // faces staged per round
+    static constexpr int FCAP = NTF >= 1024 ? NR_FWD_FCAP1024 : NTF >= 512 ? 256 : NR_FWD_FCAP256;  // faces staged per round
     static constexpr int LDS = FCAP * FREC * 16 + CAND * 4;
     static_assert(NSUB == 1 || NSUB == 2 || NSUB == 4, "forward block layout");
     // 8x8 block k of wave w: its origin (ox, oy) in the bin

@@ -56,6 +56,10 @@ ph = np.stack([t[:, :, 1] - t[:, :, 0], st, t[:, :, 3] - t[:, :, 1] - st,
 names = ["scan", "stage", "walk", "fim+flag", "shade"]
 life = t[:, :, 5] - t[:, :, 0]
 print("blocks %d; candidates per bin: zero in %.1f%%, mean %.1f over the rest" % (blocks, 100 * (nc == 0).mean(), nc[nc > 0].mean()))
+ncb = t[:, 0, 6]
+print("candidates per non-empty bin p50/p90/p99/max: %s; over 160: %.1f%%, over 512: %.1f%%" % (
+    np.percentile(ncb[ncb > 0], [50, 90, 99, 100]).astype(int), 100 * (ncb > 160).mean() / max((ncb > 0).mean(), 1e-9),
+    100 * (ncb > 512).mean() / max((ncb > 0).mean(), 1e-9)))
 for lo, hi, lab in ((0, 0, "no candidates"), (1, 10**9, "with candidates")):
     sel = (nc >= lo) & (nc <= hi)
     if not sel.any():

@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="gloo: rehearse the N > 1 path with ranks sharing GPUs (not for reported numbers)")
+    p.add_argument("--graph-steps", type=int, default=0,
+                   help="after the eager timing, time this many replays of the step captured in a HIP graph (0: skip)")
     p.add_argument("--no-gather", action="store_true",
                    help="with N > 1, skip the RCCL all_gather of the images timed after the steps (cfg4)")
     return p.parse_args()
@@ -82,11 +84,16 @@ def workload(args, rank, dev):
         vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
         tex = np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32)
         tex = torch.as_tensor(tex, device=dev).requires_grad_(True)
-        params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
-                                   faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+        vt_d, ft_d = torch.as_tensor(vt, device=dev), torch.as_tensor(ft, device=dev)
+
+        def params():
+            # built per step, as a training loop does: a batch-expanded view of the leaf texture made
+            # once would keep its autograd node alive across steps (and across a graph capture)
+            return nr.RasterizeParam(vertices_textures=vt_d[None].expand(B, -1, -1), faces_textures=ft_d,
+                                     textures=tex[None].expand(B, -1, -1, -1))
         C = 5
     else:
-        params, tex, C = nr.RasterizeParam(), None, 1
+        params, tex, C = nr.RasterizeParam, None, 1
         hp.draw_rgb, hp.draw_depth = False, False
     g = torch.as_tensor(np.random.RandomState(7).normal(size=(B, C, args.image_size, args.image_size))
                         .astype(np.float32), device=dev)
@@ -99,9 +106,26 @@ def step(w):
     w["proj"].grad = None
     if w["tex"] is not None:
         w["tex"].grad = None
-    images = rasterize_core(w["proj"], w["faces"], w["params"], w["hp"])
+    images = rasterize_core(w["proj"], w["faces"], w["params"](), w["hp"])
     images.backward(w["g"])
     return images
+
+
+def graphed(w):
+    """The same step captured in one HIP graph (torch.cuda.CUDAGraph) after a warm-up on a side
+    stream; returns its replay.  The replay launches the same kernels on the same buffers (the
+    gradients land in the graph's own .grad tensors), without the host's per-launch path and with
+    the graph's dispatch of consecutive kernels."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            step(w)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step(w)
+    return graph
 
 
 def kernel_bytes(w, args, measured=None):
@@ -259,6 +283,32 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         gather_ms = float(t.item())
 
+    graph_ms = None
+    if args.graph_steps > 0:
+        images = images.detach()  # release the last eager step's autograd graph before the capture
+        graph = graphed(w)
+        for _ in range(args.warmup):
+            graph.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.graph_steps):
+            graph.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        ge = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([ge], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            ge = float(t.item())
+        graph_ms = ge / args.graph_steps * 1e3
+        del graph
+
+    del images
     kms = time_kernels(w)
     kb, total_bytes = kernel_bytes(w, args, kms)
     dominant = max(kms, key=kms.get)
@@ -309,6 +359,10 @@ def main():
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "step_roofline_frac": round(total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
     }
+    if graph_ms is not None:
+        # the same step replayed from a captured HIP graph (not the headline value)
+        res["graph_ms_per_step"] = round(graph_ms, 4)
+        res["graph_value"] = round(world * args.batch * args.image_size ** 2 / (graph_ms * 1e-3) / 1e6, 3)
     if gather_ms is not None:
         res["gather_ms"] = round(gather_ms, 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

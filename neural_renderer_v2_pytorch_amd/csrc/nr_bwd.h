@@ -27,8 +27,11 @@ constexpr int BH = 16;                        // block height
 constexpr int HW_ = TW + 2, HH_ = BH + 2, HN = HW_ * HH_;
 constexpr int NHALO = 2 * HW_ + 2 * BH;       // 100 halo pixels
 constexpr int TWIN = 4;                       // texel window edge per face
+// pos of a pixel without a window texel: tt - POS_NONE is 16..31 for every window texel tt, so the
+// gather's footprint test (0x33 >> (d & 31)) & 1 rejects it with no separate check
+constexpr int POS_NONE = -16;
 
-// staged record: ay by ax bx | pos G_rgb[3] | gF[9] | pad (20 floats); with lights also dL/dnormal[3]
+// staged record: ay by ax bx | G_rgb[3] pos | gF[9] | pad (20 floats); with lights also dL/dnormal[3]
 // and the weights w[3] at 17..22 (24 floats)
 template <bool LIT> constexpr int srec() { return LIT ? 24 : 20; }
 constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
@@ -182,7 +185,7 @@ struct BwdPix {
     float gz[3];       // d/dz of the face corners through the depth and texture-coordinate paths
     float grgb[3];     // upstream gradient of the rgb channels
     float ay, by, ax, bx;
-    int pos;           // bilinear top-left texel relative to the face window: dx + 4 dy; -1 none
+    int pos;           // bilinear top-left texel relative to the face window: dx + 4 dy; POS_NONE none
     int wx, wy;        // face window origin (texels); INT_MIN when not windowed
     float gn[3];       // lights: dL/d(smooth normal)
 };
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         const bool inside = px < S && py < S;
         BwdPix& q = P[k];
         q.fi = inside ? fiv[k] : -1;
-        q.pos = -1;
+        q.pos = POS_NONE;
         q.wx = q.wy = INT_MIN;
         q.w[0] = q.w[1] = q.w[2] = 0.f;
         q.gz[0] = q.gz[1] = q.gz[2] = 0.f;
@@ -621,7 +624,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     for (int k = 0; k < NPX; k++) {
         float* r = rec + (16 * NPX * (lane >> 4) + 16 * k + (lane & 15)) * REC;
         reinterpret_cast<float4*>(r)[0] = make_float4(P[k].ay * P[k].ax, P[k].ay * P[k].bx, P[k].by * P[k].ax, P[k].by * P[k].bx);
-        reinterpret_cast<float4*>(r)[1] = make_float4(__int_as_float(P[k].pos), P[k].grgb[0], P[k].grgb[1], P[k].grgb[2]);
+        reinterpret_cast<float4*>(r)[1] = make_float4(P[k].grgb[0], P[k].grgb[1], P[k].grgb[2], __int_as_float(P[k].pos));
 #pragma unroll
         for (int j = 0; j < 9; j++) r[8 + j] = gF[k][j];
         if (LIT) {
@@ -695,7 +698,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             auto member = [&](int bit, bool on) {
                 const float* r = rbase + bit * REC;
                 const float4 ra = reinterpret_cast<const float4*>(r)[0];  // corner weights w00 w01 w10 w11
-                const float4 rb = reinterpret_cast<const float4*>(r)[1];  // pos G_r G_g G_b
+                const float4 rb = reinterpret_cast<const float4*>(r)[1];  // G_r G_g G_b pos (G_r, G_g a register pair)
                 const float rf = r[fsel];
                 // whole rows in registers: otherwise the compiler splits the corner select below into
                 // branches, each with its own half-row LDS read
@@ -706,15 +709,16 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                     rn = r[nsel_n];
                 }
                 // texel tt = tdx + 4 tdy is corner (d & 1, d >> 2) of the member's footprint when
-                // d = tt - pos is 0, 1, 4 or 5 (dx, dy <= 2 rule out row wrap-around)
-                const int pos = __float_as_int(rb.x);
+                // d = tt - pos is 0, 1, 4 or 5 (dx, dy <= 2 rule out row wrap-around): bits 0, 1, 4, 5
+                // of 0x33; d & 31 is 6..31 for every other d in -10..15 and for POS_NONE
+                const int pos = __float_as_int(rb.w);
                 const int d = tt - pos;
-                const bool hit = on && pos >= 0 && (unsigned)d < 6u && !(d & 2);
+                const bool hit = on && ((0x33u >> (d & 31)) & 1u);
                 const float wsel = (d & 4) ? ((d & 1) ? ra.w : ra.z) : ((d & 1) ? ra.y : ra.x);
                 const float wt = hit ? wsel : 0.f;
-                a0 += rb.y * wt;
-                a1 += rb.z * wt;
-                a2 += rb.w * wt;
+                a0 += rb.x * wt;
+                a1 += rb.y * wt;
+                a2 += rb.z * wt;
                 af += on ? rf : 0.f;
                 if (LIT) an += on ? rw * rn : 0.f;  // corner-normal gradient tt = 3 corner + axis
             };

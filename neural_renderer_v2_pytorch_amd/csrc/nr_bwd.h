@@ -141,13 +141,31 @@ __device__ __forceinline__ float upstream_one(const BwdArgs& a, const float* __r
 
 __device__ __forceinline__ float div_step(const BwdArgs& a, float x) { return a.step_pow2 ? x * a.inv_step : x / a.step; }
 
+// sum_c d[c] g[c] in channel order, as pair_dot (nr_shade.h) forms it from its differences
+__device__ __forceinline__ float diff_dot(const float* d, const float* g, int C) {
+    float s = d[0] * g[0];
+#pragma unroll
+    for (int c = 1; c < MAXC; c++)
+        if (c < C) s = s + d[c] * g[c];
+    return s;
+}
+// Each neighbour pair's channel differences serve both of its one-sided terms (axis_grad,
+// nr_shade.h): with dp = I0 - Ip, -pair_dot(Ip, I0, G0) = -sum (-dp) G0 = sum dp G0 exactly (negation
+// is exact and round-to-nearest is symmetric), and likewise for the (i - 1, i) pair; only the sign of
+// an all-zero sum can differ, which no caller observes (pick_grad compares, and it is added to gF).
 __device__ __forceinline__ float stencil(const BwdArgs& a, const float* Im, const float* I0, const float* Ip,
                                          const float* Gm, const float* G0, const float* Gp, int i, int n, int C) {
     const bool has_p = i <= n - 2, has_m = i >= 1;
-    const float r_i = has_p ? div_step(a, -pair_dot(I0, Ip, Gp, C)) : 0.f;
-    const float r_m = has_m ? div_step(a, -pair_dot(Im, I0, G0, C)) : 0.f;
-    const float l_i = has_p ? div_step(a, -pair_dot(Ip, I0, G0, C)) : 0.f;
-    const float l_m = has_m ? div_step(a, -pair_dot(I0, Im, Gm, C)) : 0.f;
+    float dp[MAXC], dm[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; c++) {
+        dp[c] = I0[c] - Ip[c];
+        dm[c] = Im[c] - I0[c];
+    }
+    const float r_i = has_p ? div_step(a, -diff_dot(dp, Gp, C)) : 0.f;
+    const float r_m = has_m ? div_step(a, -diff_dot(dm, G0, C)) : 0.f;
+    const float l_i = has_p ? div_step(a, diff_dot(dp, G0, C)) : 0.f;
+    const float l_m = has_m ? div_step(a, diff_dot(dm, Gm, C)) : 0.f;
     return pick_grad(r_i + r_m, l_m + l_i);
 }
 

@@ -211,10 +211,13 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //   (the bin's walks run 4x wider: small batches, where the grid is a few blocks per CU, and dense
 //   bins -- 300+ faces over one 8x8 block on a 50k-face torus -- no longer serialise on 4 waves).
 //   LDS face record, structure of arrays (float4 i of staged face j at s_face[i * FCAP + j]: the
-//   staging stores are lane-contiguous), 7 x float4; the pass test reads rows 0-4, the commit 1-6:
-//     0: xmin xmax ymin ymax | 1: zmin x0 y0 x1 | 2: y1 x2 y2 A=x1-x0 | 3: B=y1-y0 C=x2-x1 D=y2-y1 E=x0-x2
-//     4: F=y0-y2 k0 k1 k2 | 5: z0 z1 z2 id | 6: 1/z0 1/z1 1/z2 ok
-//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit)
+//   staging stores are lane-contiguous), 7 x float4; the pass test reads rows 0-4, the commit 2-6:
+//     0: xmin xmax ymin ymax | 1: y0 y1 x0 x1 | 2: A=x1-x0 C=x2-x1 B=y1-y0 D=y2-y1 | 3: zmin y2 x2 E=x0-x2
+//     4: F=y0-y2 k1 k2 k0 | 5: z0 z1 z2 id | 6: 1/z0 1/z1 1/z2 ok
+//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit).  The
+//   operands of edges 1 and 2 and of weights 2 and 0 sit in aligned register pairs -- (y0, y1),
+//   (x0, x1), (A, C), (B, D), (k2, k0) -- so the compiler evaluates those pairs with packed fp32
+//   instructions (each half rounded as the scalar form) and no register moves.
 constexpr int FREC = 7;  // float4 per staged face
 #ifndef NR_FWD_FCAP256
 #define NR_FWD_FCAP256 160  // staged faces per round of the 256-thread variant (8 blocks per CU need <= 20 KB of LDS; 128 -> 160: headline fwd 0.208 -> 0.195 ms)
@@ -275,12 +278,13 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
     // The rejections of .cu:94-126 are independent of each other (none changes the state), so their
     // order is free: the depth-bound reject .cu:124-126 goes first, as it is the cheapest and lets a
     // whole wave skip a face hidden behind what its pixels already hold.
-    if (depth_min < q1.x) return;
+    const float4 q3 = fr.get(e, 3);
+    if (depth_min < q3.x) return;
     // .cu:94-97 (min/max form, exact for non-NaN faces)
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
-    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
-    const float x0 = q1.y, y0 = q1.z, x1 = q1.w, y1 = q2.x, x2 = q2.y, y2 = q2.z;
-    const float A = q2.w, B = q3.x, C = q3.y, D = q3.z, E = q3.w, F = q4.x;
+    const float4 q2 = fr.get(e, 2), q4 = fr.get(e, 4);
+    const float x0 = q1.z, y0 = q1.x, x1 = q1.w, y1 = q1.y, x2 = q3.z, y2 = q3.y;
+    const float A = q2.x, B = q2.z, C = q2.y, D = q2.w, E = q3.w, F = q4.x;
     // .cu:107-116
     const float c1 = (yp - y0) * A - B * (xp - x0);
     const float c2 = (yp - y1) * C - D * (xp - x1);
@@ -294,9 +298,9 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
 #endif
     const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
     // .cu:130-139
-    float w0 = (yp * C - xp * D) + q4.y;
-    float w1 = (yp * E - xp * F) + q4.z;
-    float w2 = (yp * A - xp * B) + q4.w;
+    float w0 = (yp * C - xp * D) + q4.w;
+    float w1 = (yp * E - xp * F) + q4.y;
+    float w2 = (yp * A - xp * B) + q4.z;
     const float ws = w0 + w1 + w2;
     float zp;
     if (__float_as_int(q6.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
@@ -351,14 +355,13 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
 // minimum (a face it rejects the exact test rejects too); rows 0-5 of the record
 template <int FST>
 __device__ __forceinline__ bool face_pass(const float4* e, const FaceRows<FST>& fr, float xp, float yp, float depth_bound) {
-    const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1);
-    if (depth_bound < q1.x) return false;
+    const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1), q3 = fr.get(e, 3);
+    if (depth_bound < q3.x) return false;
     if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return false;
-    const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
-    const float x0 = q1.y, y0 = q1.z, x1 = q1.w, y1 = q2.x, x2 = q2.y, y2 = q2.z;
-    const float c1 = (yp - y0) * q2.w - q3.x * (xp - x0);  // A, B
-    const float c2 = (yp - y1) * q3.y - q3.z * (xp - x1);  // C, D
-    const float c3 = (yp - y2) * q3.w - q4.x * (xp - x2);  // E, F
+    const float4 q2 = fr.get(e, 2), q4 = fr.get(e, 4);
+    const float c1 = (yp - q1.x) * q2.x - q2.z * (xp - q1.z);  // (yp - y0) A - B (xp - x0)
+    const float c2 = (yp - q1.y) * q2.y - q2.w * (xp - q1.w);  // (yp - y1) C - D (xp - x1)
+    const float c3 = (yp - q3.y) * q3.w - q4.x * (xp - q3.z);  // (yp - y2) E - F (xp - x2)
 #if NR_FWD_PASS_BRANCHLESS
     return !(c1 * c2 < 0) && !(c2 * c3 < 0);
 #else
@@ -372,22 +375,22 @@ template <int FST, bool SLOT>
 __device__ __forceinline__ void face_commit(const float4* s_face, int slot, float xp, float yp, float near, float far,
                                             float delta, float& depth_min, int& best) {
     const float4* e = s_face + slot;
-    const float4 q1 = e[1 * FST];
+    const float4 q3 = e[3 * FST];
 #if NR_FWD_COMMIT_EAGER
-    // every row in one LDS round trip (the depth reject would otherwise wait for row 1 first)
-    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
-    asm volatile("" ::"v"(q2.w), "v"(q3.x), "v"(q3.y), "v"(q3.z), "v"(q3.w), "v"(q4.x), "v"(q4.y), "v"(q4.z));
-    asm volatile("" ::"v"(q4.w), "v"(q5.x), "v"(q5.y), "v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w));
-    if (depth_min < q1.x) return;
+    // every row in one LDS round trip (the depth reject would otherwise wait for row 3 first)
+    const float4 q2 = e[2 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
+    asm volatile("" ::"v"(q2.x), "v"(q2.y), "v"(q2.z), "v"(q2.w), "v"(q3.y), "v"(q3.w), "v"(q4.x), "v"(q4.y));
+    asm volatile("" ::"v"(q4.z), "v"(q4.w), "v"(q5.x), "v"(q5.y), "v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w));
+    if (depth_min < q3.x) return;
 #else
-    if (depth_min < q1.x) return;
-    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
+    if (depth_min < q3.x) return;
+    const float4 q2 = e[2 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
 #endif
-    const float A = q2.w, B = q3.x, C = q3.y, D = q3.z, E = q3.w, F = q4.x;
+    const float A = q2.x, B = q2.z, C = q2.y, D = q2.w, E = q3.w, F = q4.x;
     const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
-    float w0 = (yp * C - xp * D) + q4.y;
-    float w1 = (yp * E - xp * F) + q4.z;
-    float w2 = (yp * A - xp * B) + q4.w;
+    float w0 = (yp * C - xp * D) + q4.w;
+    float w1 = (yp * E - xp * F) + q4.y;
+    float w2 = (yp * A - xp * B) + q4.z;
     const float ws = w0 + w1 + w2;
     float zp;
     if (__float_as_int(q6.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {  // as face_test
@@ -424,7 +427,8 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
 template <int FST>
 __device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc, float hx, float hy) {
     const float4 q1 = e[1 * FST], q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST];
-    return nr_block_culled(q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, q4.x, xc, yc, hx, hy);
+    // x0 y0 x1 y1 x2 y2 A B C D E F
+    return nr_block_culled(q1.z, q1.x, q1.w, q1.y, q3.z, q3.y, q2.x, q2.z, q2.y, q2.w, q3.w, q4.x, xc, yc, hx, hy);
 }
 
 // one wave's walk of the n staged faces over its 8x8 block (pixel (xp, yp) per lane, pixel-centre
@@ -479,10 +483,10 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
     const float x2 = c[6], y2 = c[7], z2 = c[8];
     e[0 * FST] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
                        fmaxf(fmaxf(y0, y1), y2));
-    e[1 * FST] = make_float4(fminf(fminf(z0, z1), z2), x0, y0, x1);
-    e[2 * FST] = make_float4(y1, x2, y2, x1 - x0);
-    e[3 * FST] = make_float4(y1 - y0, x2 - x1, y2 - y1, x0 - x2);
-    e[4 * FST] = make_float4(y0 - y2, x1 * y2 - x2 * y1, x2 * y0 - x0 * y2, x0 * y1 - x1 * y0);
+    e[1 * FST] = make_float4(y0, y1, x0, x1);
+    e[2 * FST] = make_float4(x1 - x0, x2 - x1, y1 - y0, y2 - y1);
+    e[3 * FST] = make_float4(fminf(fminf(z0, z1), z2), y2, x2, x0 - x2);
+    e[4 * FST] = make_float4(y0 - y2, x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, x1 * y2 - x2 * y1);
     e[5 * FST] = make_float4(z0, z1, z2, __int_as_float(f));
     const bool ok = coord_ok(x0) && coord_ok(y0) && coord_ok(x1) && coord_ok(y1) && coord_ok(x2) && coord_ok(y2) &&
                     in_range(z0, 0x1p-20f, 0x1p20f) && in_range(z1, 0x1p-20f, 0x1p20f) &&

@@ -213,7 +213,10 @@ struct BwdPix {
 #ifndef NR_BWD_WPE1
 #define NR_BWD_WPE1 6
 #endif
-template <int FEAT, int NPX>
+// CC: the channel count as a compile-time constant (0: sh.C at run time).  With every channel present
+// (rgb + sil + depth, C = MAXC) the per-channel `c < C` guards of the loads, the LDS staging and the
+// stencil fold away, with their zero defaults and scalar branches.
+template <int FEAT, int NPX, int CC = 0>
 __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? NR_BWD_WPE1 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
     constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0, SILO = (FEAT & 4) != 0;
     // features this instantiation does not have become compile-time constants (the shared
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
     float(*s_G)[HN] = reinterpret_cast<float(*)[HN]>(s_raw + MAXC * HN);
     const int S = g.S;
-    const int C = sh.C;
+    const int C = CC ? CC : sh.C;
     const bool rgb = !SILO && (sh.draw & NR_DRAW_RGB) != 0;
     const bool want_tex = rgb && a.grad_tex != nullptr;
     constexpr bool wlate = SILO;  // silhouettes only: weights after the stencil, sparse gather
@@ -796,11 +799,16 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 #ifndef NR_BWD_NPX
 #define NR_BWD_NPX 0
 #endif
+#ifndef NR_BWD_CC
+#define NR_BWD_CC 1  // 0: no compile-time channel count (timing builds)
+#endif
 template <int FEAT>
 void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
     const bool one = NR_BWD_NPX == 1 || (NR_BWD_NPX == 0 && (long long)grid.x * grid.y < 8192);
     if (one)
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
+    else if (FEAT == 0 && sh.C == MAXC && NR_BWD_CC)
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC>), grid, dim3(NT), 0, st, ba, g, sh);
     else
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
 }

@@ -522,7 +522,9 @@ __device__ unsigned long long g_fwd_t[NR_FTIMING_MAX];
 // SHADE (NTF == 256, anti-aliasing, no lights / backgrounds): the block also shades its bin's 16x16
 // output pixels (k_shade's work, shade_quad) from the face ids it has just found, so the face-index
 // map is not read back and k_shade has no launch of its own.
-template <int NTF, bool SHADE>
+// CC (SHADE only): the channel count as a compile-time constant; CC = MAXC means rgb + sil + depth,
+// so the epilogue's draw-flag tests and per-channel guards fold away (0: sh.C / sh.draw at run time)
+template <int NTF, bool SHADE, int CC = 0>
 __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_FWDS_WPE : NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
@@ -707,6 +709,10 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         // an empty bin: every channel of its output pixels is 0 (sil, depth and rgb of background;
         // no backgrounds in this variant), as is every halo value
         Shade sh = sh_in;
+        if (CC == MAXC) {
+            sh.C = MAXC;
+            sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;
+        }
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
         if ((NTF == 256 || t < 256) && iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, halo);
@@ -721,6 +727,10 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         Shade sh = sh_in;
         sh.nl = 0;
         sh.bg = nullptr;
+        if (CC == MAXC) {
+            sh.C = MAXC;
+            sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;
+        }
         __syncthreads();
         NR_FTSTAMP(4, clock64());
         const int m = t >> 4, n = t & 15;

@@ -45,6 +45,9 @@
 #ifndef NR_FUSE_SHADE
 #define NR_FUSE_SHADE 1  // 0: k_shade always has its own launch (timing builds)
 #endif
+#ifndef NR_FWD_CC
+#define NR_FWD_CC 1  // 0: no compile-time channel count in the fused forward (timing builds)
+#endif
 #ifndef NR_FUSE_SHADE1024
 #define NR_FUSE_SHADE1024 1  // the deep-bin / small-grid 1024-thread variant shades too (threads 0-255)
 #endif
@@ -154,6 +157,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         const int rs = vertices ? FACE_REC : 9;
         if (fuse && ntf == 1024)
             hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
+        else if (fuse && sh.C == MAXC && NR_FWD_CC)  // rgb + sil + depth: compile-time channels
+            hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
         else if (fuse)
             hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,

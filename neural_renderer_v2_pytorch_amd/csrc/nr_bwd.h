@@ -224,6 +224,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     Shade sh = sh_in;
     if (!LIT) sh.nl = 0;
     if (!BG) sh.bg = nullptr;
+    if (CC == MAXC) sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;  // the only 5-channel render
     constexpr int REC = srec<LIT>();
     __shared__ __attribute__((aligned(16))) float s_raw[bwd_lds<LIT>() / 4];
     float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);

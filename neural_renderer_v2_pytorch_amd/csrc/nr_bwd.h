@@ -215,7 +215,8 @@ struct BwdPix {
 #endif
 // CC: the channel count as a compile-time constant (0: sh.C at run time).  With every channel present
 // (rgb + sil + depth, C = MAXC) the per-channel `c < C` guards of the loads, the LDS staging and the
-// stencil fold away, with their zero defaults and scalar branches.
+// stencil fold away, with their zero defaults and scalar branches; that instantiation is launched
+// only with anti-aliasing and a power-of-two raster (both folded too).
 template <int FEAT, int NPX, int CC = 0>
 __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? NR_BWD_WPE1 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
     constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0, SILO = (FEAT & 4) != 0;
@@ -224,7 +225,12 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     Shade sh = sh_in;
     if (!LIT) sh.nl = 0;
     if (!BG) sh.bg = nullptr;
-    if (CC == MAXC) sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;  // the only 5-channel render
+    if (CC == MAXC) {
+        // the only 5-channel render; launched only with anti-aliasing and a power-of-two raster
+        sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;
+        a.aa = 1;
+        a.step_pow2 = 1;
+    }
     constexpr int REC = srec<LIT>();
     __shared__ __attribute__((aligned(16))) float s_raw[bwd_lds<LIT>() / 4];
     float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
@@ -808,7 +814,7 @@ void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, con
     const bool one = NR_BWD_NPX == 1 || (NR_BWD_NPX == 0 && (long long)grid.x * grid.y < 8192);
     if (one)
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
-    else if (FEAT == 0 && sh.C == MAXC && NR_BWD_CC)
+    else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2 && NR_BWD_CC)
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC>), grid, dim3(NT), 0, st, ba, g, sh);
     else
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);

@@ -157,9 +157,6 @@ __device__ __forceinline__ Face empty_face() {
     return f;
 }
 
-// torch.maximum / torch.minimum / min(-2) / max(-2) semantics: NaN propagates
-__device__ __forceinline__ float t_max(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a > b ? a : b); }
-__device__ __forceinline__ float t_min(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : (a < b ? a : b); }
 
 // ---- exact division without the scaling / fix-up steps --------------------------------------
 // gfx950 lowers an IEEE binary32 a / b to
@@ -296,12 +293,17 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
         else
             s.num[j] = ((w[0] * u0) / s.zq[0] + (w[1] * u1) / s.zq[1]) + (w[2] * u2) / s.zq[2];
         s.pr[j] = s.num[j] * s.dt;
-        s.lo[j] = t_min(t_min(u0, u1), u2);
-        s.hm[j] = t_max(t_max(u0, u1), u2) - eps;
-        s.pc[j] = t_max(s.pr[j], s.lo[j]);
+        // torch.minimum / maximum and min(-2) / max(-2) as gfx950's NaN-propagating v_minimum3_f32 /
+        // v_maximum3_f32 (one instruction each).  Against (a < b ? a : b) with NaN propagation they differ only in the sign of a
+        // zero result when the operands are +0 and -0, which leaves every value sample_texture yields
+        // unchanged: floor(-0) = -0, x - floor(x) = +0 and 1 - x = 1 either way, and the gradient
+        // paths compare these values (sign-blind).
+        s.lo[j] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(u0, u1), u2);
+        s.hm[j] = __builtin_elementwise_maximum(__builtin_elementwise_maximum(u0, u1), u2) - eps;
+        s.pc[j] = __builtin_elementwise_maximum(s.pr[j], s.lo[j]);
     }
-    s.x = t_min(s.pc[0], s.hm[0]);
-    s.y = t_min(s.pc[1], s.hm[1]);
+    s.x = __builtin_elementwise_minimum(s.pc[0], s.hm[0]);
+    s.y = __builtin_elementwise_minimum(s.pc[1], s.hm[1]);
     s.x0 = floorf(s.x);
     s.y0 = floorf(s.y);
     s.x1 = s.x0 + 1;

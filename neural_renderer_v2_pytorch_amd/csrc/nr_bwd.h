@@ -386,6 +386,8 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             wfast = face_weights(xp, yp, f, q.w);
         }
         const float* w = q.w;
+        float dz[3];  // w_k / z_k, shared by the depth and (FACE_ZQ_EQ faces) the texture sampling
+        face_dz(f, w, wfast, dz);
         float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
         if (rgb && !(NR_ABLATE & 128)) {
             TexSample s;
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
             // bilinear: images = sum_i wt_i T_i -> textures (staged below) and weights (gw)
             float gw[4];
-            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s, Gt, gw);
+            sample_texture(f, w, wfast, fuv, sh.tv, bt, sh.eps, s, Gt, gw, dz);
             r = s.rgb[0];
             gg = s.rgb[1];
             bb = s.rgb[2];
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
         }
         if ((sh.draw & NR_DRAW_DEPTH) && !(NR_ABLATE & 256)) {
-            dep = depth_value(f, w, wfast);
+            dep = depth_from_dz(dz, wfast);
             // depth channel gradient: selected from the registers with compile-time indices (a
             // runtime-indexed register array would go to scratch)
             const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);

@@ -123,6 +123,7 @@ __device__ __forceinline__ int range_hi(int p) { return p >> 16; }
 constexpr int FACE_REC = 16;
 constexpr int FACE_FAST_XYZ = 1;  // x, y in {0} u [2^-20, 2^20], |z| in [2^-20, 2^20]
 constexpr int FACE_FAST_ZQ = 2;   // |z + 1e-10| in [2^-20, 2^20]
+constexpr int FACE_ZQ_EQ = 4;     // z + 1e-10 == z for every corner (|z| >= ~2^-6): w / (z + 1e-10) == w / z
 struct Face {
     float x0, y0, z0, x1, y1, z1, x2, y2, z2;
     float rz0, rz1, rz2, rq0, rq1, rq2;
@@ -268,19 +269,30 @@ __device__ __forceinline__ FaceUV load_face_uv(const float* __restrict__ uv) {
 // wfast: face_weights took its exact-division path.
 // G (optional, backward): upstream gradient of the rgb channels; then gw[i] = sum_c G[c] T_i[c] for
 // the 4 bilinear texels, from the texel values loaded here (no second load)
+// dz (optional): w_k / z_k from face_dz; on a FACE_ZQ_EQ face these are the w_k / (z_k + 1e-10) the
+// sampling needs, bit for bit, and its own three divisions are skipped
 __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], bool wfast, const FaceUV& uvr,
                                                const TexView& tv, int bt, float eps, TexSample& s,
-                                               const float* G = nullptr, float* gw = nullptr) {
+                                               const float* G = nullptr, float* gw = nullptr, const float* dz = nullptr) {
     const float4 uva = uvr.a, uvb = uvr.b;
     const float uvs[6] = {uva.x, uva.y, uva.z, uva.w, uvb.x, uvb.y};
     const bool fast = wfast && (f.flags & FACE_FAST_ZQ) && __float_as_int(uvb.z) != 0;
     const float z[3] = {f.z0, f.z1, f.z2};
     const float rq[3] = {f.rq0, f.rq1, f.rq2};
-    float st = 0.f;
+    float tq[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         s.zq[k] = z[k] + 1e-10f;
-        const float t = (fast ? div_nr(w[k], s.zq[k], rq[k]) : w[k] / s.zq[k]) + 1e-10f;
+        tq[k] = dz ? dz[k] : 0.f;
+    }
+    if (!dz || !(f.flags & FACE_ZQ_EQ)) {  // skipped when every lane's face has z + 1e-10 == z
+#pragma unroll
+        for (int k = 0; k < 3; k++) tq[k] = fast ? div_nr(w[k], s.zq[k], rq[k]) : w[k] / s.zq[k];
+    }
+    float st = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float t = tq[k] + 1e-10f;
         st = (k == 0) ? t : st + t;
     }
     s.dt = fast ? recip_exact(st) : 1.f / st;
@@ -367,12 +379,30 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
     }
 }
 
-// compute_depth_map (rasterize.py:80-88) for a foreground pixel
-__device__ __forceinline__ float depth_value(const Face& f, const float w[3], bool wfast) {
-    if (wfast) {  // weights in {0} u [2^-84, 1], |z| in [2^-20, 2^20]
-        return recip_exact((div_nr(w[0], f.z0, f.rz0) + div_nr(w[1], f.z1, f.rz1)) + div_nr(w[2], f.z2, f.rz2));
+// w_k / z_k of a foreground pixel (the exact shortened division on the fast path: weights in
+// {0} u [2^-84, 1], |z| in [2^-20, 2^20]), shared by the depth and, on FACE_ZQ_EQ faces, the texture
+// sampling.  The shortened form can give +0 where IEEE gives -0 for a zero weight; both callers add
+// these terms to nonzero ones.
+__device__ __forceinline__ void face_dz(const Face& f, const float w[3], bool wfast, float dz[3]) {
+    if (wfast) {
+        dz[0] = div_nr(w[0], f.z0, f.rz0);
+        dz[1] = div_nr(w[1], f.z1, f.rz1);
+        dz[2] = div_nr(w[2], f.z2, f.rz2);
+    } else {
+        dz[0] = w[0] / f.z0;
+        dz[1] = w[1] / f.z1;
+        dz[2] = w[2] / f.z2;
     }
-    return 1.f / ((w[0] / f.z0 + w[1] / f.z1) + w[2] / f.z2);
+}
+// compute_depth_map (rasterize.py:80-88) for a foreground pixel, from face_dz's terms
+__device__ __forceinline__ float depth_from_dz(const float dz[3], bool wfast) {
+    const float sum = (dz[0] + dz[1]) + dz[2];
+    return wfast ? recip_exact(sum) : 1.f / sum;
+}
+__device__ __forceinline__ float depth_value(const Face& f, const float w[3], bool wfast) {
+    float dz[3];
+    face_dz(f, w, wfast, dz);
+    return depth_from_dz(dz, wfast);
 }
 
 struct Shade {
@@ -488,9 +518,11 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
     if (fi >= 0 && shade_needs_face(sh)) {
         float w[3];
         const bool wfast = face_weights(xp, yp, f, w);
+        float dz[3];
+        face_dz(f, w, wfast, dz);
         if (R) {
             TexSample s;
-            sample_texture(f, w, wfast, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s);
+            sample_texture(f, w, wfast, fuv, sh.tv, sh.tv.sb ? b : 0, sh.eps, s, nullptr, nullptr, dz);
             r = s.rgb[0];
             gg = s.rgb[1];
             bb = s.rgb[2];
@@ -503,7 +535,7 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
                 bb = bb * cw[2];
             }
         }
-        if (sh.draw & NR_DRAW_DEPTH) dep = depth_value(f, w, wfast);
+        if (sh.draw & NR_DRAW_DEPTH) dep = depth_from_dz(dz, wfast);
     }
     if (R && sh.bg) {  // fg * rgb + (1 - fg) * bg (chainer rasterize.py:576)
         float bgc[3];

@@ -49,16 +49,17 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                     c[3 * k + 2] = vb[vi * 3 + 2];
                 }
                 // 16-float record: corners, rcp_nr(z_k), rcp_nr(z_k + 1e-10), range flags (see Face)
-                bool fxyz = true, fzq = true;
+                bool fxyz = true, fzq = true, zeq = true;
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
                     fxyz = fxyz && coord_ok(c[3 * k]) && coord_ok(c[3 * k + 1]) && in_range(c[3 * k + 2], 0x1p-20f, 0x1p20f);
                     fzq = fzq && in_range(c[3 * k + 2] + 1e-10f, 0x1p-20f, 0x1p20f);
+                    zeq = zeq && (c[3 * k + 2] + 1e-10f == c[3 * k + 2]);
                 }
 #ifdef NR_NO_FASTDIV
                 const int flags = 0;  // timing build: IEEE divisions everywhere
 #else
-                const int flags = (fxyz ? FACE_FAST_XYZ : 0) | (fzq ? FACE_FAST_ZQ : 0);
+                const int flags = (fxyz ? FACE_FAST_XYZ : 0) | (fzq ? FACE_FAST_ZQ : 0) | (zeq ? FACE_ZQ_EQ : 0);
 #endif
                 float4* rec = reinterpret_cast<float4*>(s_frec + t * FACE_REC);
                 rec[0] = make_float4(c[0], c[1], c[2], c[3]);

@@ -346,6 +346,9 @@ __device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& 
 #ifndef NR_FWD_COMMIT_EAGER
 #define NR_FWD_COMMIT_EAGER 1
 #endif
+#ifndef NR_FWD_PASS_UNI
+#define NR_FWD_PASS_UNI 1  // the walk keeps the pass test's outcome as a wave mask (0: face_pass per lane)
+#endif
 #ifndef NR_FWD_PASS_BRANCHLESS
 #define NR_FWD_PASS_BRANCHLESS 1  // edge tests without branches (car fwd 0.849 -> 0.838 ms; headline even)
 #endif
@@ -457,7 +460,33 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
             const float4* e = s_face + slot;
             FaceRows<FST> fr;
             fr.load(e);
-#if NR_FWD_DEFER
+#if NR_FWD_DEFER && NR_FWD_PASS_UNI
+            // face_pass with its outcome kept as a wave mask: the depth and bbox tests of every lane
+            // form one mask, the edge tests run only when a lane is left (a uniform branch), and the
+            // pending slot is set from the mask directly (no per-lane boolean to rebuild a ballot from)
+            const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1), q3 = fr.get(e, 3);
+            // (bitwise & and |: no short-circuit control flow)
+            const unsigned long long pre = __ballot((!(depth_min < q3.x)) &
+                                                    !((xp < q0.x) | (xp > q0.y) | (yp < q0.z) | (yp > q0.w)));
+            unsigned long long cov = 0;
+            if (pre) {
+                const float4 q2 = fr.get(e, 2), q4 = fr.get(e, 4);
+                const float c1 = (yp - q1.x) * q2.x - q2.z * (xp - q1.z);
+                const float c2 = (yp - q1.y) * q2.y - q2.w * (xp - q1.w);
+                const float c3 = (yp - q3.y) * q3.w - q4.x * (xp - q3.z);
+                cov = __ballot(!((c1 * c2 < 0) | (c2 * c3 < 0))) & pre;
+            }
+            if (cov & occ) {  // commit first where this face would queue behind a pending one
+                if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
+                pend = -1;
+                occ = 0;
+            }
+            {
+                int sv = slot;
+                asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(pend) : "v"(pend), "v"(sv), "s"(cov));
+            }
+            occ |= cov;
+#elif NR_FWD_DEFER
             const bool pass = face_pass<FST>(e, fr, xp, yp, depth_min);
             const unsigned long long cov = __ballot(pass);
             if (cov & occ) {  // commit first where this face would queue behind a pending one

@@ -389,6 +389,37 @@ def test_headline_sampled_items_vs_oracle(oracle_mod, dev):
         close_grads(pv.grad[i:i + 1], pc.grad, "item %d grad vertices" % i)
 
 
+def test_tiny_depth_faces_vs_oracle(oracle_mod, dev):
+    """Faces whose z + 1e-10 does not round to z (FACE_ZQ_EQ clear: the texture sampling divides by
+    z + 1e-10 itself) beside faces where it does (the depth's w / z terms are reused), mixed within
+    waves: every even vertex's z scaled by 2^-12 (near lowered to 1e-5), a 32-item batch through the
+    fused C = 5 forward and backward, items 0 and 31 against the CPU oracle."""
+    B = 32
+    proj, f = _ico_batch(4, B, dev)
+    proj = proj.clone()
+    proj[:, 0::2, 2] *= 2.0 ** -12
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex_cpu = torch.rand(tex.shape, generator=torch.Generator().manual_seed(5))
+    tex = tex_cpu.to(dev)
+    pv = proj.to(dev).requires_grad_(True)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+    img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(near=1e-5),
+                                  return_face_index=True)
+    assert bool((fim >= 0).any())
+    g = torch.randn(img.shape, generator=torch.Generator().manual_seed(12))
+    img.backward(g.to(dev))
+    for i in (0, B - 1):
+        pc = proj[i:i + 1].clone().requires_grad_(True)
+        ref, internals = oracle_mod.rasterize_core(pc, f, image_size=256, near=1e-5,
+                                                   vertices_textures=torch.as_tensor(vt)[None], faces_textures=ft,
+                                                   textures=tex_cpu[None], return_internals=True)
+        ref.backward(g[i:i + 1])
+        assert np.array_equal(fim[i].cpu().numpy(), internals["fim"][0].numpy()), "item %d fim" % i
+        close_images(img[i:i + 1], ref, "item %d images" % i)
+        close_grads(pv.grad[i:i + 1], pc.grad, "item %d grad vertices" % i)
+
+
 @pytest.mark.parametrize("mode", ["sil", "depth", "rgba", "rgbsd"])
 def test_fused_forward_shading_matches_separate_shade(dev, mode):
     """A 32-item batch at 256^2 AA takes the forward with shading fused into the face-index kernel

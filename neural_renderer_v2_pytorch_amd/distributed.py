@@ -18,9 +18,13 @@ import torch.distributed as dist
 
 def world(group=None):
     """(rank, world size) within `group` (the default group when None); (0, 1) without a
-    process group."""
+    process group.  A rank outside `group` gets a ValueError: torch reports it as rank -1, which
+    the shard arithmetic would otherwise silently use."""
     if dist.is_available() and dist.is_initialized():
-        return dist.get_rank(group), dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        if rank < 0:
+            raise ValueError("this process (global rank %d) is not a member of the given group" % dist.get_rank())
+        return rank, dist.get_world_size(group)
     return 0, 1
 
 
@@ -68,14 +72,16 @@ def gather_images(local, batch_size=None, group=None):
 def allreduce_shared_grads(params, group=None):
     """Sum the gradients of parameters shared by every rank's items (in place).
 
-    Every rank issues the same collectives in the same order: a parameter whose .grad is None on
-    this rank (an empty shard, or a branch this rank did not take) contributes zeros, and its
-    .grad is materialised, so no rank skips an all_reduce the others enter."""
+    Every rank issues the same collectives in the same order: a parameter that requires grad but
+    whose .grad is None on this rank (an empty shard, or a branch this rank did not take)
+    contributes zeros, and its .grad is materialised, so no rank skips an all_reduce the others
+    enter.  Parameters that do not require grad (frozen) are skipped on every rank alike and keep
+    .grad None, so optimisers (weight decay, momentum) leave them alone."""
     _, ws = world(group)
     if ws == 1:
         return
     for p in params:
-        if p is None:
+        if p is None or not p.requires_grad:
             continue
         if p.grad is None:
             p.grad = torch.zeros_like(p)

@@ -117,7 +117,33 @@ def mask_foreground(data, face_index_map):
 
 # ------------------------------------------------------------------------------------------------
 # the fused path
-_faces_checked = {}
+class _TensorCache:
+    """Small LRU of results derived from device index tensors (the faces checks and the vertex
+    adjacency), keyed by (storage address, version counter, shape, ...).  Each entry keeps its
+    source tensor alive, so its storage -- hence the address in the key -- cannot be freed and
+    reused by another tensor while the entry lives; the version counter catches in-place edits.
+    A caller alternating a few meshes (several objects, or train / validation sets) keeps hitting:
+    no device-to-host copy and no host sync per call, so such steps stay graph-capturable."""
+
+    def __init__(self, size=8):
+        import collections
+        self.size = size
+        self.entries = collections.OrderedDict()
+
+    def get(self, key):
+        hit = self.entries.get(key)
+        if hit is not None:
+            self.entries.move_to_end(key)
+        return hit
+
+    def put(self, key, value):
+        self.entries[key] = value
+        self.entries.move_to_end(key)
+        while len(self.entries) > self.size:
+            self.entries.popitem(last=False)
+
+
+_faces_checked = _TensorCache()
 
 
 def _faces_i32(faces, device, bound, what):
@@ -135,29 +161,26 @@ def _faces_i32(faces, device, bound, what):
         return f.to(dtype=torch.int32).contiguous().to(device, non_blocking=False)
     reuse = f.dtype == torch.int32 and f.is_contiguous() and f.device == device
     f = f.to(device=device, dtype=torch.int32).contiguous()
-    key = (f.data_ptr(), f._version, f.shape[0], bound)
-    hit = _faces_checked.get(what)
-    if f.numel() and not (reuse and hit is not None and hit[0] == key):
+    key = (f.data_ptr(), f._version, f.shape[0], bound, f.device)
+    if f.numel() and not (reuse and _faces_checked.get(key) is not None):
         lo, hi = int(f.min()), int(f.max())
         if lo < 0 or hi >= bound:
             raise IndexError("%s index out of range [0, %d): min %d max %d" % (what, bound, lo, hi))
         if reuse:
-            # the entry holds the tensor: its storage, hence the address in the key, cannot be
-            # freed and reused by another tensor while the entry is live
-            _faces_checked[what] = (key, f)
+            _faces_checked.put(key, f)
     return f
 
 
-_adjacency = {}
+_adjacency = _TensorCache()
 
 
 def _vertex_adjacency(faces_i32, V):
     """CSR vertex -> face corners (3 f + k) for the backward's vertex gather, built on the host
     with a stable sort (deterministic summation order) and cached per (storage, version)."""
     key = (faces_i32.data_ptr(), faces_i32._version, faces_i32.shape[0], V, faces_i32.device)
-    hit = _adjacency.get("faces")
-    if hit is not None and hit[0] == key:
-        return hit[1], hit[2]
+    hit = _adjacency.get(key)
+    if hit is not None:
+        return hit[0], hit[1]
     import numpy as np
     flat = faces_i32.reshape(-1).cpu().numpy().astype(np.int64)
     order = np.argsort(flat, kind="stable").astype(np.int32)
@@ -166,20 +189,20 @@ def _vertex_adjacency(faces_i32, V):
     np.cumsum(counts, out=offsets[1:])
     off = torch.as_tensor(offsets, device=faces_i32.device)
     ent = torch.as_tensor(order, device=faces_i32.device)
-    _adjacency["faces"] = (key, off, ent, faces_i32)  # keep faces_i32 alive: its storage is the key
+    _adjacency.put(key, (off, ent, faces_i32))  # keep faces_i32 alive: its storage is the key
     return off, ent
 
 
-_normal_adj = {}
+_normal_adj = _TensorCache()
 
 
 def _normal_adjacency(faces_i32, V):
     """CSR vertex -> its distinct faces, ascending (the one-hot [F, V] matrix of
     rasterize.py:173-179: a face counts once per vertex), cached per faces tensor."""
     key = (faces_i32.data_ptr(), faces_i32._version, faces_i32.shape[0], V, faces_i32.device)
-    hit = _normal_adj.get("faces")
-    if hit is not None and hit[0] == key:
-        return hit[1], hit[2]
+    hit = _normal_adj.get(key)
+    if hit is not None:
+        return hit[0], hit[1]
     import numpy as np
     f = faces_i32.cpu().numpy().astype(np.int64)
     F = f.shape[0]
@@ -189,7 +212,7 @@ def _normal_adjacency(faces_i32, V):
     np.cumsum(counts, out=offsets[1:])
     off = torch.as_tensor(offsets, device=faces_i32.device)
     ent = torch.as_tensor(pairs[:, 1].astype(np.int32), device=faces_i32.device)
-    _normal_adj["faces"] = (key, off, ent, faces_i32)
+    _normal_adj.put(key, (off, ent, faces_i32))
     return off, ent
 
 

@@ -3,6 +3,7 @@
 Meshes:
   * icosphere(level)  -- level 4: V=2562, F=5120 (the headline "~5k-face mesh"), radius 0.9
   * torus(nu, nv)     -- 250x100: V=25000, F=50000 (config 5)
+  * subdivide(v, f, vt, ft) -- one midpoint subdivision (the ShapeNet car 3644 -> 14576 faces, config 3)
 Scenes: per-item Gaussian vertex jitter (seed 1000+b) and per-item viewpoint
 get_points_from_angles(2.732, U(-30,30), U(0,360)) (seed 2000+b); faces shared across the batch.
 """
@@ -57,6 +58,30 @@ def torus(nu=250, nv=100, major=0.65, minor=0.25):
     d = i * nv + (j + 1) % nv
     f = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)], 0)
     return v, f.astype(np.int32)
+
+
+def subdivide(v, f, vt=None, ft=None):
+    """Midpoint subdivision: every triangle into 4 (shared edge midpoints, computed in float64);
+    the same on the uv mesh when given.  SURVEY.md section 8d: the car 4e49873... (F=3644) once
+    subdivided is the "ShapeNet car ~15k faces" of BASELINE config 3 (F=14576)."""
+    def split(verts, faces):
+        cache, out_v, nf = {}, [tuple(x) for x in verts], []
+
+        def mid(a, b):
+            key = (min(a, b), max(a, b))
+            if key not in cache:
+                out_v.append(tuple((np.asarray(out_v[a], np.float64) + np.asarray(out_v[b], np.float64)) / 2))
+                cache[key] = len(out_v) - 1
+            return cache[key]
+        for a, b, c in faces:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            nf += [(a, ab, ca), (b, bc, ab), (c, ca, bc), (ab, bc, ca)]
+        return np.asarray(out_v, np.float32), np.asarray(nf, np.int32)
+    v2, f2 = split(v, f)
+    if vt is None:
+        return v2, f2
+    vt2, ft2 = split(vt, ft)
+    return v2, f2, vt2, ft2
 
 
 def viewpoints(batch_size, distance=2.732, seed_base=2000):

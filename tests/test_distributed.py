@@ -121,8 +121,19 @@ def _group_worker(rank, world_size, port, out_dir):
         p = torch.zeros(4, requires_grad=True)
         if rank != 1:
             (p * float(rank + 1)).sum().backward()
-        ndist.allreduce_shared_grads([p])
+        frozen = torch.ones(3)  # requires_grad False: skipped on every rank, .grad stays None
+        ndist.allreduce_shared_grads([p, frozen, None])
+        assert frozen.grad is None
         res["grad"] = p.grad.numpy()
+        if rank == 1:  # not in `group`: a clear error instead of shard math with rank -1
+            try:
+                ndist.world(group)
+            except ValueError:
+                res["outside_raises"] = np.array(1)
+            try:
+                ndist.gather_images(torch.zeros(1, 3), group=group)
+            except ValueError:
+                res["gather_outside_raises"] = np.array(1)
         np.savez(os.path.join(out_dir, "g%d.npz" % rank), **res)
     finally:
         dist.destroy_process_group()
@@ -134,6 +145,8 @@ def test_gloo_subgroup_and_missing_grad(tmp_path):
     for r in range(3):
         got = np.load(str(tmp_path / ("g%d.npz" % r)))
         np.testing.assert_array_equal(got["grad"], np.full(4, 1.0 + 3.0, np.float32))
+        if r == 1:
+            assert int(got["outside_raises"]) == 1 and int(got["gather_outside_raises"]) == 1
         if r != 1:
             np.testing.assert_array_equal(got["gathered"], want)
             np.testing.assert_array_equal(got["gathered_known"], want)

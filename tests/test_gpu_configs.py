@@ -1,0 +1,327 @@
+"""BASELINE.json's other single-GPU configurations, and the k_raster_fwd code paths only they reach,
+checked against the CPU oracle on the GPU (through the C ABI, one batched call each).
+
+  cfg2  teapot (2464 faces), B=4, 256^2 AA, rgb + silhouettes + depth, forward + backward: every
+        item against the oracle.
+  cfg3  ShapeNet car 4e49873... once subdivided (14576 faces), B=64, 256^2 AA, the car's own
+        texture atlas shared by the batch, rgba, forward + backward: sampled items against the
+        oracle (the car's deep bins: up to thousands of candidate faces per 32x32 bin, the
+        1024-thread forward with its edge cull, and the backward's direct texel atomics).
+  cfg5  torus 250x100 (50000 faces) at 512^2 (1024^2 internal) through Renderer.render_silhouettes:
+        face-index map bit-exact against the brute-force oracle (the 1024-thread forward's
+        multi-word bin masks, nwords = 1563 > 1024), silhouette gradients; and the 200-step
+        example2-style Adam loop.
+  k_raster_fwd<256>, two branches the headline never takes:
+        * bins with more candidates than one 160-face staging round (the static-quadrant walk
+          with per-pixel state carried across rounds, and the fused shading through s_fim): a
+          distant ico-sphere, B = 32;
+        * bin masks wider than 256 words (the wbase loop): 9000 faces, B = 32.
+  the backward's background-tile skip next to foreground pixels on 32-pixel bin borders, with the
+  halo cache on (skip active) and off.
+
+Tolerances as in test_gpu_parity.py: face-index map bit-exact; images |d| <= 1e-5 + 1e-5 |ref|;
+gradients |d| <= 1e-4 max|ref| + 1e-4 |ref|.  The oracle runs the reference's brute-force scan
+(oracle/nr_oracle.c, OpenMP) and its torch-CPU stages on the sampled items.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import neural_renderer_v2_pytorch_amd as nr
+from neural_renderer_v2_pytorch_amd import rasterize as nrr
+from neural_renderer_v2_pytorch_amd import synthetic
+from test_gpu_parity import close_grads, close_images
+
+pytestmark = pytest.mark.gpu
+
+DATA = os.path.join(os.path.dirname(__file__), "data")
+CAR = os.path.join(DATA, "4e49873292196f02574b5684eaec43e9", "model.obj")
+
+
+def _scene(v, B, seed=0):
+    """Per-item jittered vertices and viewpoints, projected on the CPU."""
+    vb = torch.as_tensor(synthetic.jittered(v, B, seed_base=1000 + seed))
+    eyes = torch.as_tensor(synthetic.viewpoints(B, seed_base=2000 + seed))
+    return synthetic.project(vb, eyes).contiguous()
+
+
+def _oracle(oracle_mod, proj, f, items, image_size, g, tex=None, vt=None, ft=None, **kw):
+    """The oracle on items `items` of a batch: (images, fim, grad vertices, grad of the shared
+    texture summed over these items)."""
+    n = len(items)
+    pc = proj[list(items)].detach().cpu().clone().requires_grad_(True)
+    extra = {}
+    tx = None
+    if tex is not None:
+        tx = tex.detach().cpu().clone().requires_grad_(True)
+        extra = dict(vertices_textures=torch.as_tensor(vt)[None].expand(n, -1, -1), faces_textures=ft,
+                     textures=tx[None].expand(n, -1, -1, -1))
+    ref, internals = oracle_mod.rasterize_core(pc, f, image_size=image_size, return_internals=True, **extra, **kw)
+    ref.backward(g[list(items)].cpu())
+    return ref.detach(), internals["fim"].numpy(), pc.grad, (tx.grad if tx is not None else None)
+
+
+def _textured(F, B, dev, seed):
+    vt, ft, tex = nr.create_textures(F, texture_size=4)
+    tex_cpu = torch.rand(tex.shape, generator=torch.Generator().manual_seed(seed))
+    leaf = tex_cpu.to(dev).requires_grad_(True)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=leaf[None].expand(B, -1, -1, -1))
+    return params, leaf, tex_cpu, vt, ft
+
+
+def _bin_candidates(proj, f, S):
+    """Per (item, 32x32 bin): faces whose pixel bbox (+-1 px) touches the bin -- the bin-mask
+    candidate count of k_face_setup, conservatively."""
+    fv = proj[:, torch.as_tensor(f).long()].numpy()            # [B, F, 3, 3]
+    px = (fv[..., 0] * S + S - 1) / 2                            # pixel coordinate of each corner
+    py = (fv[..., 1] * S + S - 1) / 2
+    nb = (S + 31) // 32
+    lo_x = np.clip(np.floor(px.min(-1)) - 1, 0, S - 1) // 32
+    hi_x = np.clip(np.ceil(px.max(-1)) + 1, 0, S - 1) // 32
+    lo_y = np.clip(np.floor(py.min(-1)) - 1, 0, S - 1) // 32
+    hi_y = np.clip(np.ceil(py.max(-1)) + 1, 0, S - 1) // 32
+    counts = np.zeros((fv.shape[0], nb, nb), np.int64)
+    for b in range(fv.shape[0]):
+        for yb in range(nb):
+            for xb in range(nb):
+                counts[b, yb, xb] = int(np.sum((lo_x[b] <= xb) & (xb <= hi_x[b]) & (lo_y[b] <= yb) & (yb <= hi_y[b])))
+    return counts
+
+
+def test_cfg2_teapot_full_size_vs_oracle(oracle_mod, dev):
+    """BASELINE cfg2 at its full size: teapot B=4, 256^2 output (512^2 internal), rgb + sil + depth,
+    one batched forward + backward; every item against the oracle (the shared texture's gradient
+    against the oracle's sum over the four items)."""
+    v, f = nr.load_obj(os.path.join(DATA, "teapot.obj"))
+    B = 4
+    proj = _scene(v, B)
+    params, tex, tex_cpu, vt, ft = _textured(f.shape[0], B, dev, 41)
+    g = torch.randn((B, 5, 256, 256), generator=torch.Generator().manual_seed(42))
+    pv = proj.to(dev).requires_grad_(True)
+    img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
+                                  return_face_index=True)
+    img.backward(g.to(dev))
+    ref, rfim, rgv, rgt = _oracle(oracle_mod, proj, f, range(B), 256, g, tex_cpu, vt, ft)
+    assert np.array_equal(fim.cpu().numpy(), rfim), int((fim.cpu().numpy() != rfim).sum())
+    close_images(img, ref, "cfg2 images")
+    close_grads(pv.grad, rgv, "cfg2 grad vertices")
+    close_grads(tex.grad, rgt, "cfg2 grad textures")
+
+
+def test_cfg3_car_subdivided_vs_oracle(oracle_mod, dev):
+    """BASELINE cfg3: the ShapeNet car once subdivided (14576 faces), B=64, 256^2 AA, textured rgba
+    with the car's own atlas shared by the batch (tests_torch/test_rasterize.py:43-81 renders this
+    car).  One batched forward + backward; items 0, 31, 63 against the oracle: face-index map
+    bit-exact, images, vertex gradients.  A second backward of the same graph with the upstream
+    gradient kept on those three items only gives the shared atlas gradient, checked against the
+    oracle's sum over them."""
+    v, f, vt, ft, tex = nr.load_obj(CAR, load_textures=True)
+    v, f, vt, ft = synthetic.subdivide(v, f, vt, ft)
+    assert f.shape[0] == 14576
+    B, s = 64, 256
+    proj = _scene(v, B)
+    tex_cpu = torch.as_tensor(np.ascontiguousarray(tex)).float()
+    assert tex_cpu.shape[0] == 3
+    leaf = tex_cpu.to(dev).requires_grad_(True)
+    params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=leaf[None].expand(B, -1, -1, -1))
+    hp = nr.RasterizeHyperparam(image_size=s, draw_depth=False)
+    pv = proj.to(dev).requires_grad_(True)
+    img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, hp, return_face_index=True)
+    assert img.shape == (B, 4, s, s)
+    counts = _bin_candidates(proj[:4], f, 2 * s)
+    assert counts.max() > 512, counts.max()  # deep bins: more than one 512-face staging round
+    g = torch.randn(img.shape, generator=torch.Generator().manual_seed(43))
+    img.backward(g.to(dev), retain_graph=True)
+    assert torch.isfinite(pv.grad).all() and torch.isfinite(leaf.grad).all()
+    items = (0, 31, 63)
+    ref, rfim, rgv, rgt = _oracle(oracle_mod, proj, f, items, s, g, tex_cpu, vt, ft, draw_depth=False)
+    for k, i in enumerate(items):
+        assert np.array_equal(fim[i].cpu().numpy(), rfim[k]), "item %d fim: %d px" % (
+            i, int((fim[i].cpu().numpy() != rfim[k]).sum()))
+        close_images(img[i:i + 1], ref[k:k + 1], "cfg3 item %d images" % i)
+        close_grads(pv.grad[i:i + 1], rgv[k:k + 1], "cfg3 item %d grad vertices" % i)
+    gm = torch.zeros_like(g)
+    gm[list(items)] = g[list(items)]
+    leaf.grad = None
+    img.backward(gm.to(dev))
+    close_grads(leaf.grad, rgt, "cfg3 grad textures (items 0, 31, 63)")
+
+
+def _torus_renderer():
+    ren = nr.Renderer()
+    ren.image_size = 512
+    ren.viewpoints = nr.get_points_from_angles(2.732, 30, -15)
+    return ren
+
+
+def test_cfg5_torus_1024_vs_oracle(oracle_mod, dev):
+    """BASELINE cfg5's render: the 50000-face torus at 512^2 with anti-aliasing (1024^2 internal)
+    through Renderer.render_silhouettes (examples_pytorch/example2.py:72-78).  The Renderer's
+    output equals rasterize_silhouettes of its own camera transform bit for bit; that render's
+    face-index map is bit-exact against the brute-force oracle (.cu:82-149 over all 50000 faces:
+    1563 mask words per bin, past the 1024-thread forward's one-word-per-thread staging), and its
+    silhouette gradients match the oracle's.  The gradient reaching the mesh through the camera
+    equals the camera backward of that projected-vertex gradient."""
+    v, f = synthetic.torus(250, 100)
+    faces = torch.as_tensor(f, device=dev)
+    ren = _torus_renderer()
+    verts = torch.as_tensor(v[None], device=dev).requires_grad_(True)
+    img = ren.render_silhouettes(verts, faces)
+    assert img.shape == (1, 512, 512)
+    g = torch.randn(img.shape, generator=torch.Generator().manual_seed(44))
+    img.backward(g.to(dev))
+    with torch.no_grad():
+        proj = ren.transform_vertices(verts).detach()
+    pv = proj.clone().requires_grad_(True)
+    hp = nr.RasterizeHyperparam(image_size=512)
+    hp.draw_rgb = hp.draw_depth = False
+    img2, fim = nrr.rasterize_core(pv, faces, nr.RasterizeParam(), hp, return_face_index=True)
+    assert torch.equal(img2[:, 0], img.detach())
+    img2[:, 0].backward(g.to(dev))
+    ref, rfim, rgv, _ = _oracle(oracle_mod, proj.cpu(), f, [0], 512, g[:, None], draw_rgb=False, draw_depth=False)
+    assert np.array_equal(fim.cpu().numpy(), rfim), int((fim.cpu().numpy() != rfim).sum())
+    assert int((rfim >= 0).sum()) > 100000
+    close_images(img2, ref, "cfg5 silhouettes")
+    close_grads(pv.grad, rgv, "cfg5 grad projected vertices")
+    vv = torch.as_tensor(v[None], device=dev).requires_grad_(True)
+    gv, = torch.autograd.grad(ren.transform_vertices(vv), vv, pv.grad)
+    close_grads(verts.grad, gv, "cfg5 grad vertices through the camera")
+
+
+def test_cfg5_torus_adam_loop(dev):
+    """BASELINE cfg5's loop: 200 fwd+bwd steps with an Adam update of the torus's vertices toward a
+    silhouette of the torus scaled by 1.1 (tools/bench_configs.py cfg5, example2.py:17-78): every
+    loss finite, and the loss falls below 1 % of its start."""
+    v, f = synthetic.torus(250, 100)
+    faces = torch.as_tensor(f, device=dev)
+    ren = _torus_renderer()
+    with torch.no_grad():
+        target = ren.render_silhouettes(torch.as_tensor(v[None] * 1.1, device=dev), faces)
+    verts = torch.nn.Parameter(torch.as_tensor(v[None], device=dev))
+    opt = torch.optim.Adam([verts], lr=0.001)
+    losses = []
+    for _ in range(200):
+        opt.zero_grad()
+        loss = ((ren.render_silhouettes(verts, faces) - target) ** 2).sum()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+    print("cfg5 loop loss: first %.1f, step 100 %.1f, last %.1f" % (losses[0], losses[100], losses[-1]))
+    assert all(math.isfinite(x) for x in losses)
+    # measured on an MI355X: 11610 -> 16.9 (step 100) -> 4.1 (step 200)
+    assert losses[0] > 5000 and losses[-1] < 0.01 * losses[0], (losses[0], losses[-1])
+
+
+def test_fwd256_multi_round_bins_vs_oracle(oracle_mod, dev):
+    """k_raster_fwd<256, true, 5> with bins deeper than one staging round: an ico-sphere (5120
+    faces) shrunk to a ~16-pixel disc, B = 32 at 256^2 AA.  The launch takes the 256-thread variant
+    (8192 blocks, 20 faces per bin on average), but the disc's bins hold hundreds of candidates, so
+    they walk static quadrants over several 160-face rounds and shade through the s_fim hand-over.
+    Items 0, 13, 31 against the oracle: face-index map, images, vertex gradients."""
+    B = 32
+    v, f = synthetic.icosphere(4)
+    proj = _scene(v, B).clone()
+    proj[..., 0] = proj[..., 0] * 0.06 + 0.013
+    proj[..., 1] = proj[..., 1] * 0.06 - 0.021
+    S = 512
+    nbins = (S // 32) ** 2
+    assert B * nbins >= 8192 and f.shape[0] / nbins < 40  # nr_raster.hip: the 256-thread variant
+    counts = _bin_candidates(proj, f, S)
+    assert (counts.reshape(B, -1).max(1) > 2 * 160).all(), counts.reshape(B, -1).max(1)
+    params, tex, tex_cpu, vt, ft = _textured(f.shape[0], B, dev, 45)
+    pv = proj.to(dev).requires_grad_(True)
+    img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
+                                  return_face_index=True)
+    g = torch.randn(img.shape, generator=torch.Generator().manual_seed(46))
+    img.backward(g.to(dev))
+    items = (0, 13, 31)
+    ref, rfim, rgv, _ = _oracle(oracle_mod, proj, f, items, 256, g, tex_cpu, vt, ft)
+    for k, i in enumerate(items):
+        assert int((rfim[k] >= 0).sum()) > 150
+        assert np.array_equal(fim[i].cpu().numpy(), rfim[k]), "item %d fim: %d px" % (
+            i, int((fim[i].cpu().numpy() != rfim[k]).sum()))
+        close_images(img[i:i + 1], ref[k:k + 1], "item %d images" % i)
+        close_grads(pv.grad[i:i + 1], rgv[k:k + 1], "item %d grad vertices" % i)
+
+
+def test_fwd256_wide_bin_masks_vs_oracle(oracle_mod, dev):
+    """k_raster_fwd<256, true, 5> with more than 256 mask words per bin (the candidate expansion's
+    wbase loop): a 90x50 torus, 9000 faces = 282 words, B = 32 at 256^2 AA (35 faces per bin on
+    average: still the 256-thread variant).  Items 0 and 31 against the oracle."""
+    B = 32
+    v, f = synthetic.torus(90, 50)
+    F = f.shape[0]
+    S = 512
+    nbins = (S // 32) ** 2
+    assert (F + 31) // 32 > 256 and B * nbins >= 8192 and F / nbins < 40
+    proj = _scene(v, B)
+    params, tex, tex_cpu, vt, ft = _textured(F, B, dev, 47)
+    pv = proj.to(dev).requires_grad_(True)
+    img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
+                                  return_face_index=True)
+    g = torch.randn(img.shape, generator=torch.Generator().manual_seed(48))
+    img.backward(g.to(dev))
+    items = (0, 31)
+    ref, rfim, rgv, _ = _oracle(oracle_mod, proj, f, items, 256, g, tex_cpu, vt, ft)
+    for k, i in enumerate(items):
+        assert np.array_equal(fim[i].cpu().numpy(), rfim[k]), "item %d fim: %d px" % (
+            i, int((fim[i].cpu().numpy() != rfim[k]).sum()))
+        close_images(img[i:i + 1], ref[k:k + 1], "item %d images" % i)
+        close_grads(pv.grad[i:i + 1], rgv[k:k + 1], "item %d grad vertices" % i)
+
+
+def test_bin_border_faces_background_skip(oracle_mod, dev):
+    """The backward skips a 32x16 tile whose 32x32 bin has no candidate face and reads foreground
+    pixels' neighbour values from the halo cache.  Small triangles hug the right and bottom borders
+    of every other bin (a checkerboard; the rest are empty), their edges at -1.5 ... +1.5 px from
+    the border, B = 2, 256^2 without anti-aliasing, textured rgb + sil + depth: gradients with the
+    halo cache (skip active) and without (every tile recomputed), and both against the oracle."""
+    S, B = 256, 2
+    r = np.random.RandomState(49)
+    offs = [-1.5, -1.0, -0.5, -0.01, 0.0, 0.01, 0.5, 1.0, 1.5]
+    tris = []
+    for by in range(S // 32):
+        for bx in range(S // 32):
+            if (bx + by) % 2:
+                continue
+            d = offs[(bx * 3 + by) % len(offs)]
+            x0, y0 = 32 * bx + 18 + r.uniform(-2, 2), 32 * by + 17 + r.uniform(-2, 2)
+            tris.append([(x0, y0), (32 * (bx + 1) - 0.5 + d, 32 * by + 21.3), (32 * bx + 23.7, 32 * (by + 1) - 0.5 + d)])
+            tris.append([(32 * (bx + 1) - 0.5 + d, 32 * by + 8.2), (32 * (bx + 1) - 0.5 + d, 32 * by + 27.9),
+                         (32 * bx + 25.1, 32 * by + 16.0)])
+    tris = np.asarray(tris, np.float64)                          # [F, 3, 2] pixel coordinates
+    F = tris.shape[0]
+    ndc = (2 * tris + 1 - S) / S
+    verts = np.zeros((B, F * 3, 3), np.float32)
+    for b in range(B):
+        z = r.uniform(1.0, 3.0, size=(F, 3))
+        verts[b, :, :2] = ndc.reshape(-1, 2) * (1 + 0.002 * b)
+        verts[b, :, 2] = z.reshape(-1)
+    f = np.arange(F * 3, dtype=np.int32).reshape(F, 3)
+    proj = torch.as_tensor(verts)
+    g = torch.randn((B, 5, S, S), generator=torch.Generator().manual_seed(50))
+    out = {}
+    for halo in (True, False):
+        nrr._HALO_CACHE = halo
+        try:
+            params, tex, tex_cpu, vt, ft = _textured(F, B, dev, 51)
+            pv = proj.to(dev).requires_grad_(True)
+            img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params,
+                                          nr.RasterizeHyperparam(image_size=S, anti_aliasing=False), return_face_index=True)
+            img.backward(g.to(dev))
+            out[halo] = (img.detach(), fim, pv.grad, tex.grad)
+        finally:
+            nrr._HALO_CACHE = True
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
+    ref, rfim, rgv, rgt = _oracle(oracle_mod, proj, f, range(B), S, g, tex_cpu, vt, ft, anti_aliasing=False)
+    assert np.array_equal(out[True][1].cpu().numpy(), rfim)
+    assert int((rfim >= 0).sum()) > 2000
+    for halo in (True, False):
+        close_images(out[halo][0], ref, "images (halo %d)" % halo)
+        close_grads(out[halo][2], rgv, "grad vertices (halo %d)" % halo)
+        close_grads(out[halo][3], rgt, "grad textures (halo %d)" % halo)

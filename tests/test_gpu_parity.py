@@ -119,19 +119,23 @@ def test_silhouettes_teapot(golden, dev):
 
 
 def test_renderer_silhouettes_teapot(golden, dev):
-    """Renderer path (look_at + perspective on the GPU, then rasterize): the camera transform runs on
-    the GPU's BLAS, so projected vertices may differ from the CPU reference in the last ulp."""
+    """Renderer path (look_at + perspective fused on the GPU, then rasterize) against the
+    reference's golden, which projected the vertices with the torch CPU composition.  Observed on
+    an MI355X: no silhouette pixel flips and the vertex gradient's relative L1 error is 1.7e-8, so
+    the bounds are the strict ones: a bit-exact image and the per-element gradient tolerance."""
     d = golden("teapot_sil")
     ren = nr.Renderer()
     ren.anti_aliasing = False
     ren.viewpoints = nr.get_points_from_angles(2.732, 0, 0)
     v = torch.as_tensor(d["vertices"], device=dev).requires_grad_(True)
     img = ren.render_silhouettes(v, torch.as_tensor(d["faces"], device=dev))
-    diff = (img.detach().cpu() != torch.as_tensor(d["images"])).float().mean().item()
-    assert diff < 1e-3, diff
+    flips = int((img.detach().cpu() != torch.as_tensor(d["images"])).sum())
     img.backward(torch.as_tensor(d["grad_up"], device=dev))
-    g, ref = v.grad.cpu()[2], torch.as_tensor(d["grad_vertices"])[2]
-    assert float((g - ref).abs().sum() / ref.abs().sum()) < 2e-2
+    g, ref = v.grad.cpu(), torch.as_tensor(d["grad_vertices"])
+    l1 = float((g - ref).abs().sum() / ref.abs().sum())
+    print("Renderer teapot: %d of %d silhouette pixels flip; grad L1 rel %.3g" % (flips, img.numel(), l1))
+    assert flips == 0, flips
+    close_grads(g, ref, "Renderer teapot grad vertices")
 
 
 def test_depth_teapot(golden, dev):
@@ -988,3 +992,99 @@ def test_backward_workspace_zeroed_by_forward(dev):
     for i in range(2):
         torch.testing.assert_close(out[True][0][i], out[False][0][i], rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(out[True][1][i], 2 * out[True][0][i], rtol=1e-5, atol=1e-6)
+
+
+def test_two_meshes_alternating_in_one_hip_graph(dev):
+    """Faces checks and adjacencies are cached per faces tensor in a small LRU (rasterize.py
+    _TensorCache): a caller alternating two meshes pays the host-side checks once per mesh, never
+    per call.  Proof that no call syncs with the host: after one eager step per mesh, a step that
+    renders and differentiates mesh A, then mesh B, then A again is captured in ONE HIP graph
+    (a device-to-host copy or a .cpu() inside the capture would raise) and replayed; the replayed
+    images equal the eager ones bit for bit and the gradients agree within the tolerance."""
+    s = 64
+    meshes = []
+    for level, B in ((3, 2), (2, 3)):
+        proj, f = _ico_batch(level, B, dev)
+        meshes.append((proj.detach().to(dev).requires_grad_(True), torch.as_tensor(f, device=dev)))
+    g = [torch.randn((p.shape[0], 5, s, s), generator=torch.Generator().manual_seed(70 + i)).to(dev)
+         for i, (p, _) in enumerate(meshes)]
+    tex = torch.rand((3, 16, 16), generator=torch.Generator().manual_seed(72)).to(dev)
+
+    def render(i):
+        pv, faces = meshes[i]
+        hp = nr.RasterizeHyperparam(image_size=s)
+        hp.draw_rgb = False
+        img = nrr.rasterize_core(pv, faces, nr.RasterizeParam(), hp)
+        img.backward(g[i][:, :img.shape[1]])
+        return img
+
+    def step():
+        return [render(0), render(1), render(0)]
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            for pv, _ in meshes:
+                pv.grad = None
+            eager = [x.detach().clone() for x in step()]
+    torch.cuda.current_stream().wait_stream(side)
+    eager_g = [pv.grad.clone() for pv, _ in meshes]
+    for pv, _ in meshes:
+        pv.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = step()
+    graph.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(out, eager):
+        assert torch.equal(a, b)
+    for (pv, _), ge in zip(meshes, eager_g):
+        close_grads(pv.grad, ge, "graph grad vertices")
+    assert len(nrr._faces_checked.entries) >= 2 and len(nrr._adjacency.entries) >= 2
+
+
+def test_car_renderer_render_batch(oracle_mod, dev):
+    """The car (tests_torch/test_rasterize.py:43-81's scene) through Renderer.render at B = 4 views:
+    the output equals rasterize_rgba of the Renderer's own camera transform bit for bit, and that
+    render matches the oracle on the same projected vertices (face-index map bit-exact, images,
+    vertex and texture gradients).  The fused camera itself is checked against the reference's
+    torch composition in float64 by test_camera_transform_vs_torch."""
+    from neural_renderer_v2_pytorch_amd import camera
+    v, f, vt, ft, tex = nr.load_obj(os.path.join(os.path.dirname(__file__), "data", "4e49873292196f02574b5684eaec43e9",
+                                                 "model.obj"), load_textures=True)
+    B = 4
+    eyes = torch.as_tensor(np.stack([nr.get_points_from_angles(2.5, 10 * i, -90 + 40 * i) for i in range(B)]),
+                           dtype=torch.float32, device=dev)
+    ren = nr.Renderer()
+    ren.draw_backside = False
+    ren.viewpoints = eyes
+    mesh = torch.as_tensor(v[None], device=dev).requires_grad_(True)
+    atlas = torch.as_tensor(tex, device=dev).requires_grad_(True)
+    vt_d, ft_d, f_d = torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1), torch.as_tensor(ft, device=dev), \
+        torch.as_tensor(f, device=dev)
+    img = ren.render(mesh.expand(B, -1, -1), f_d, vt_d, ft_d, atlas[None].expand(B, -1, -1, -1))
+    assert img.shape == (B, 4, 256, 256)
+    with torch.no_grad():
+        proj = camera.camera_transform(mesh.expand(B, -1, -1), eyes, perspective=True, angle=30)
+    hp = nr.RasterizeHyperparam(image_size=256, draw_backside=False)
+    params = nr.RasterizeParam(vertices_textures=vt_d, faces_textures=ft_d, textures=atlas.detach()[None].expand(B, -1, -1, -1))
+    assert torch.equal(nr.rasterize_rgba(proj, f_d, params, hp), img.detach())
+    pv = proj.clone().requires_grad_(True)
+    tx = atlas.detach().clone().requires_grad_(True)
+    params = nr.RasterizeParam(vertices_textures=vt_d, faces_textures=ft_d, textures=tx[None].expand(B, -1, -1, -1))
+    img2, fim = nrr.rasterize_core(pv, f_d, params, nr.RasterizeHyperparam(image_size=256, draw_backside=False,
+                                                                          draw_depth=False), return_face_index=True)
+    g = torch.randn(img2.shape, generator=torch.Generator().manual_seed(74))
+    img2.backward(g.to(dev))
+    pc = proj.cpu().clone().requires_grad_(True)
+    tc = torch.as_tensor(tex).clone().requires_grad_(True)
+    ref, internals = oracle_mod.rasterize_core(pc, f, image_size=256, draw_backside=False, draw_depth=False,
+                                               vertices_textures=torch.as_tensor(vt)[None].expand(B, -1, -1),
+                                               faces_textures=ft, textures=tc[None].expand(B, -1, -1, -1),
+                                               return_internals=True)
+    ref.backward(g)
+    assert np.array_equal(fim.cpu().numpy(), internals["fim"].numpy())
+    close_images(img2, ref, "car Renderer.render images")
+    close_grads(pv.grad, pc.grad, "car grad projected vertices")
+    close_grads(tx.grad, tc.grad, "car grad textures")

@@ -120,6 +120,68 @@ def test_no_cpu_fallback():
         nr.rasterize_silhouettes(v, torch.as_tensor([[0, 1, 2]]), nr.RasterizeParam(), nr.RasterizeHyperparam())
 
 
+def test_differentiation_cpu_golden(golden):
+    """BASELINE cfg1: the reference's Differentiation runs on CPU tensors (differentiation.py:6-36).
+    The package's CPU branch against the golden KAT made by the reference itself, bit for bit."""
+    d = golden("diff_kat")
+    for i in range(3):
+        images = torch.as_tensor(d["images%d" % i])
+        coords = torch.zeros(images.shape[:3] + (2,), requires_grad=True)
+        y = nr.differentiation(images, coords)
+        assert y is images or torch.equal(y, images)
+        y.backward(torch.as_tensor(d["grad%d" % i]))
+        assert torch.equal(coords.grad, torch.as_tensor(d["grad_xy%d" % i])), i
+
+
+def test_differentiation_cpu_reference_procedure():
+    """tests_torch/test_differentiation.py:10-65 verbatim procedure, on CPU tensors (cfg1)."""
+    r = np.random.RandomState(0)
+    images = torch.as_tensor(r.normal(size=(10, 32, 32, 3)).astype('float32'))
+    x = np.tile(np.arange(32).astype('float32')[None, None, :, None], (10, 32, 1, 1))
+    y = np.tile(np.arange(32).astype('float32')[None, :, None, None], (10, 1, 32, 1))
+    coordinates = ((np.concatenate((x, y), axis=-1) / 31) * 2 - 1) * 31. / 32.
+    noise = torch.as_tensor(r.normal(size=(10, 32, 32, 3)).astype('float32'))
+    step = 2 / 32.
+    coordinates = torch.tensor(coordinates, requires_grad=True)
+    torch.sum(nr.differentiation(images, coordinates) * noise).backward()
+    g = coordinates.grad
+    for _ in range(100):
+        yi, xi = r.randint(1, 31), r.randint(1, 31)
+        pairs = []
+        for axis in (1, 0):
+            for sgn in (1, -1):
+                im = images.clone()
+                if axis == 1:
+                    im[:, yi - sgn, xi] = images[:, yi, xi]
+                    im[:, yi, xi] = images[:, yi + sgn, xi]
+                else:
+                    im[:, yi, xi - sgn] = images[:, yi, xi]
+                    im[:, yi, xi] = images[:, yi, xi + sgn]
+                gg = ((im - images) * noise).sum((1, 2, 3)) / step
+                pairs.append(torch.min(gg, torch.zeros_like(gg)))
+        gy = torch.max(pairs[0].abs(), pairs[1].abs())
+        gx = torch.max(pairs[2].abs(), pairs[3].abs())
+        assert torch.allclose(gy, g[:, yi, xi, 1].abs().to(gy.dtype), rtol=1e-4, atol=0)
+        assert torch.allclose(gx, g[:, yi, xi, 0].abs().to(gx.dtype), rtol=1e-4, atol=0)
+
+
+def test_cfg1_cpu_pipeline():
+    """BASELINE cfg1 end to end on the CPU: teapot -> look_at -> perspective -> differentiation,
+    with gradients reaching the vertices through the projection (the rasterizer itself is GPU only)."""
+    v, f = nr.load_obj(os.path.join(DATA, "teapot.obj"))
+    verts = torch.as_tensor(v[None]).requires_grad_(True)
+    eye = torch.as_tensor(nr.get_points_from_angles(2.732, 0, 90), dtype=torch.float32)[None]
+    proj = nr.perspective(nr.look_at(verts, eye))
+    S = 16
+    img = torch.zeros((1, S, S, 3))
+    # a smooth image whose values depend on the projected vertices, then the soft gradient
+    img = img + proj[:, :S * S, :].reshape(1, S, S, 3)
+    coords = proj[:, :S * S, :2].reshape(1, S, S, 2)
+    out = nr.differentiation(img, coords)
+    (out * torch.linspace(-1, 1, out.numel()).reshape(out.shape)).sum().backward()
+    assert verts.grad is not None and torch.isfinite(verts.grad).all() and float(verts.grad.abs().sum()) > 0
+
+
 def test_product_never_imports_oracle():
     pkg = os.path.join(ROOT, "neural_renderer_v2_pytorch_amd")
     for dirpath, _, files in os.walk(pkg):

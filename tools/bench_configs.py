@@ -31,26 +31,7 @@ from neural_renderer_v2_pytorch_amd import synthetic  # noqa: E402
 DATA = os.path.join(ROOT, "tests", "data")
 
 
-def subdivide(v, f, vt=None, ft=None):
-    """Midpoint subdivision: every triangle into 4 (shared edge midpoints); the same on the uv mesh."""
-    def split(verts, faces):
-        cache, out_v, nf = {}, [tuple(x) for x in verts], []
-
-        def mid(a, b):
-            key = (min(a, b), max(a, b))
-            if key not in cache:
-                out_v.append(tuple((np.asarray(out_v[a], np.float64) + np.asarray(out_v[b], np.float64)) / 2))
-                cache[key] = len(out_v) - 1
-            return cache[key]
-        for a, b, c in faces:
-            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
-            nf += [(a, ab, ca), (b, bc, ab), (c, ca, bc), (ab, bc, ca)]
-        return np.asarray(out_v, np.float32), np.asarray(nf, np.int32)
-    v2, f2 = split(v, f)
-    if vt is None:
-        return v2, f2
-    vt2, ft2 = split(vt, ft)
-    return v2, f2, vt2, ft2
+subdivide = synthetic.subdivide  # (moved to the package: tests use it too)
 
 
 def median_step(fn, steps, warmup):

@@ -145,11 +145,11 @@ typedef struct NrRasterArgs {
      * backward then sample (one 16-B load per bilinear corner); kept by the caller from the forward
      * to the backward.  NULL = sample `textures` directly (same results). */
     float* textures_packed;
-    /* optional: the backward's workspace (nr_backward_workspace_bytes), allocated before the forward.
-     * The forward zeroes its first bwd_workspace_bytes bytes (the backward's accumulators) from the
-     * face-setup launch, and nr_rasterize_backward called with this same pointer as its workspace
-     * skips its own zero fill. Name it in one backward only: after a backward its accumulators are
-     * no longer zero. NULL = the backward zero-fills its workspace. */
+    /* optional, read by nr_rasterize_forward only: the backward's workspace
+     * (nr_backward_workspace_bytes), allocated before the forward.  The forward zeroes its first
+     * bwd_workspace_bytes bytes (the backward's accumulators) from the face-setup launch; the caller
+     * may then pass workspace_zeroed = 1 to the ONE nr_rasterize_backward call that uses this
+     * workspace next (after a backward its accumulators are no longer zero).  NULL = nothing zeroed. */
     void* bwd_workspace;
     size_t bwd_workspace_bytes;
 } NrRasterArgs;
@@ -177,9 +177,14 @@ NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num
 /* Backward of nr_rasterize_forward for upstream grad_images [B, C, s, s] (contiguous), given the
  * state the forward saved in `args`.  Writes grad_vertices [B, V, 3] and, with NR_DRAW_RGB and
  * grad_textures != NULL, grad_textures [Bt, 3, H, W] contiguous with Bt = (tex_stride_b ? B : 1)
- * (the batch total when the textures are shared).  Needs args->vertex_offsets/vertex_faces. */
+ * (the batch total when the textures are shared).  Needs args->vertex_offsets/vertex_faces.
+ * workspace_zeroed: per call, 1 when the caller guarantees the workspace's accumulators are zero
+ * (the forward zeroed them through NrRasterArgs.bwd_workspace and no backward has used it since):
+ * the backward then skips its own zero fill; 0 = the backward zero-fills (always correct).  A
+ * second backward over the same forward state must pass 0. */
 NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
-                                 float* grad_textures, void* workspace, size_t workspace_bytes, void* stream);
+                                 float* grad_textures, void* workspace, size_t workspace_bytes, int workspace_zeroed,
+                                 void* stream);
 
 /* The gradients that only the rgb channels carry and nr_rasterize_backward does not produce, for the
  * same forward state and upstream grad_images:

@@ -88,7 +88,7 @@ def lib():
     L.nr_differentiation_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
     L.nr_rasterize_forward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p]
     L.nr_rasterize_backward.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p,
-                                        c_size_t, c_void_p]
+                                        c_size_t, c_int, c_void_p]
     L.nr_rasterize_backward_params.argtypes = [ctypes.POINTER(NrRasterArgs), c_void_p, c_void_p, c_void_p, c_void_p]
     L.nr_camera_forward.argtypes = [ctypes.POINTER(NrCameraArgs), c_void_p, c_void_p]
     L.nr_camera_backward.argtypes = [ctypes.POINTER(NrCameraArgs), c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,

@@ -78,7 +78,7 @@ __global__ void k_selftest_div(const float* __restrict__ a, const float* __restr
 extern "C" {
 
 const char* nr_last_error(void) { return g_err.c_str(); }
-int nr_version(void) { return 2; }
+int nr_version(void) { return 3; }
 size_t nr_raster_args_size(void) { return sizeof(NrRasterArgs); }
 
 int nr_num_channels(int draw_flags) {
@@ -306,7 +306,7 @@ size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num_vertic
 }
 
 int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float* grad_vertices, float* grad_textures,
-                          void* workspace, size_t workspace_bytes, void* stream) {
+                          void* workspace, size_t workspace_bytes, int workspace_zeroed, void* stream) {
     int e = validate_raster(a, false);
     if (e) return e;
     if (a->batch_size == 0) {
@@ -345,8 +345,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     float* gU = lit ? (float*)(w + align_up((size_t)a->batch_size * a->num_faces * 9 * 4)) : nullptr;
     // gU is fully written by k_vnormal_bwd; the accumulators before it start at zero
     const size_t zero_bytes = lit ? (size_t)((char*)gU - (char*)workspace) : need;
-    // ... unless the forward zeroed them (NrRasterArgs.bwd_workspace names this workspace)
-    const bool prezeroed = a->bwd_workspace && a->bwd_workspace == workspace && a->bwd_workspace_bytes >= zero_bytes;
+    // ... unless the caller states, for this call, that the forward zeroed them (NrRasterArgs.bwd_workspace)
+    const bool prezeroed = workspace_zeroed != 0;
     if (zero_bytes > 0 && !prezeroed && hipMemsetAsync(workspace, 0, zero_bytes, st) != hipSuccess)
         return check_launch("hipMemsetAsync");
     BwdArgs ba;

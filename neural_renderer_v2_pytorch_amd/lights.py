@@ -1,6 +1,8 @@
 """Light records (reference lights.py:4-39): same classes, attributes and defaults.  rasterize_core
-turns a list of them into per-item records for the HIP shading (NrRasterArgs.lights); gradients
-flow to the vertices through the normals, not to the light parameters."""
+turns a list of them into per-item records for the HIP shading (NrRasterArgs.lights), built with
+differentiable torch ops: gradients flow to the vertices through the normals and, through
+nr_rasterize_backward_params, to the light colours, directions and specular exponents that
+require them (pinned by the param_grads_* goldens)."""
 import torch
 
 

@@ -431,11 +431,11 @@ class Rasterize(torch.autograd.Function):
         bg = (backgrounds, gbg) if backgrounds is not None else None
         a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo, ctx.light, bg,
                   tex4=ctx.tex4)
-        if prezeroed:  # the forward zeroed it: no fill in the backward
-            a.bwd_workspace, a.bwd_workspace_bytes = ws.data_ptr(), ws.numel()
         with torch.cuda.device(dev):
+            # workspace_zeroed = 1 only for the first backward after the forward zeroed it (no fill)
             _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),
-                                               ws.numel(), _lib.stream_of(vertices)), "nr_rasterize_backward")
+                                               ws.numel(), int(prezeroed), _lib.stream_of(vertices)),
+                       "nr_rasterize_backward")
         if gt is not None:
             # the Function's texture input is [B, 3, H, W], or the single [3, H, W] / [1, 3, H, W]
             # source of a shared texture (see rasterize_core): same element count as gt either way

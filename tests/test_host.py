@@ -96,7 +96,7 @@ def test_library_exports_every_header_symbol():
     L = ctypes.CDLL(_lib.LIB_PATH)
     for name in declared:
         assert hasattr(L, name), name
-    assert _lib.lib().nr_version() == 2
+    assert _lib.lib().nr_version() == 3
     # the ctypes mirror of NrRasterArgs has the C layout
     assert _lib.lib().nr_raster_args_size() == ctypes.sizeof(_lib.NrRasterArgs)
     assert _lib.lib().nr_num_channels(7) == 5 and _lib.lib().nr_num_channels(2) == 1
@@ -233,3 +233,19 @@ def test_edge_cull_is_exact_on_host(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     m = re.match(r"checked (\d+) culled (\d+) passes-in-culled (\d+)", out.stdout)
     assert m and int(m.group(3)) == 0 and int(m.group(2)) > int(m.group(1)) // 4, out.stdout
+
+
+def test_tensor_cache_lru():
+    """rasterize._TensorCache: a small LRU keyed by (storage, version, ...); hits refresh an
+    entry, the least recently used entry leaves first, and entries keep their source alive."""
+    from neural_renderer_v2_pytorch_amd.rasterize import _TensorCache
+    c = _TensorCache(size=2)
+    a, b, d = torch.zeros(3), torch.ones(3), torch.full((3,), 2.0)
+    ka, kb, kd = [(t.data_ptr(), t._version) for t in (a, b, d)]
+    c.put(ka, a)
+    c.put(kb, b)
+    assert c.get(ka) is a       # refreshes a: b is now the oldest
+    c.put(kd, d)
+    assert c.get(kb) is None and c.get(ka) is a and c.get(kd) is d
+    a.add_(1)                   # an in-place edit bumps the version: a new key
+    assert c.get((a.data_ptr(), a._version)) is None

@@ -39,13 +39,17 @@ def parse():
     p.add_argument("--level", type=int, default=4, help="ico-sphere subdivision level (4 -> 5120 faces)")
     p.add_argument("--mode", choices=["rgbsd", "sil"], default="rgbsd")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-seconds", type=float, default=30.0,
+                   help="cap on the CPU baseline's timed work (it times the whole batch when that fits)")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="gloo: rehearse the N > 1 path with ranks sharing GPUs (not for reported numbers)")
     p.add_argument("--graph-steps", type=int, default=0,
                    help="after the eager timing, time this many replays of the step captured in a HIP graph (0: skip)")
     p.add_argument("--no-gather", action="store_true",
                    help="with N > 1, skip the RCCL all_gather of the images timed after the steps (cfg4)")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the rocprofv3 --pmc passes that measure the roofline's HBM traffic and VALU share")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled pass (internal)
     return p.parse_args()
 
 
@@ -199,14 +203,36 @@ def copy_ceiling_gbs(dev, nbytes=1 << 30, reps=10):
     return gbs
 
 
+def host_cpu():
+    """(model name, logical CPUs of the machine, CPUs this process may run on)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, allowed
+
+
 def cpu_baseline(args, budget_s):
     """The CPU oracle (C brute-force kernels with OpenMP + torch CPU stages of rasterize_core), timed
-    on this host on whole items of the same workload until ~budget_s seconds have been spent."""
+    on this host over the same workload's items, one at a time, until the whole batch is done or
+    ~budget_s seconds have been spent.  Threads: every CPU this process may use, capped by the
+    OMP_NUM_THREADS allotment when the environment sets one (the GPU box presets 16 host threads
+    per GPU)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     import neural_renderer_v2_pytorch_amd as nr
     from neural_renderer_v2_pytorch_amd import synthetic
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    model, ncpu, allowed = host_cpu()
+    preset = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(allowed, preset) if preset > 0 else allowed
     torch.set_num_threads(threads)
     os.environ["OMP_NUM_THREADS"] = str(threads)
     v, f = synthetic.icosphere(args.level)
@@ -231,14 +257,78 @@ def cpu_baseline(args, budget_s):
         t_total += time.perf_counter() - t0
         done += 1
     mpx = done * args.image_size ** 2 / t_total / 1e6
-    return dict(value=mpx, unit="Mpixels/s", cores=threads, kind="port",
-                sample="%d item(s) of the headline workload (1 item = 256^2 output, 512^2 internal, %d faces, "
-                       "fwd+bwd), %.1f s; oracle/nr_oracle.c brute force (OpenMP) + torch-CPU stages"
-                       % (done, f.shape[0], t_total))
+    why = ("all %d CPUs this process may use" % threads if threads == allowed else
+           "the OMP_NUM_THREADS=%d allotment of the %d CPUs this process may use" % (threads, allowed))
+    return dict(value=mpx, unit="Mpixels/s", cores=threads, kind="port", cpu_model=model, nproc=ncpu,
+                cpus_allowed=allowed, threads_why=why,
+                sample="%d of the %d items of the headline batch (1 item = 256^2 output, 512^2 internal, %d faces, "
+                       "fwd+bwd), %.1f s; oracle/nr_oracle.c brute force (OpenMP, %d threads) + torch-CPU stages"
+                       % (done, args.batch, f.shape[0], t_total, threads))
+
+
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE"))
+VALU_PEAK_INSTS = 1024 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMD-32 at 2.4 GHz, 2 cycles each (MI355X_MICROARCH.md)
+
+
+def pmc_passes(args, timeout_s=240):
+    """The roofline's HBM traffic and VALU share, measured in this run: three rocprofv3 --pmc passes
+    (FETCH_SIZE, WRITE_SIZE and the SQ/GRBM counters each in a pass of their own, as
+    MI355X_MICROARCH.md's HBM section prescribes), each over a child process that runs 3 steps of
+    the same workload plus the 1 GiB -> 1 GiB calibration stream; tools/pmc_traffic.py turns the
+    counters into bytes per launch.  Returns (summary or None, note)."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_traffic
+    d = tempfile.mkdtemp(prefix="nr_pmc_")
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--steps", "3", "--warmup", "1",
+             "--batch", str(args.batch), "--image-size", str(args.image_size), "--level", str(args.level),
+             "--mode", args.mode]
+    try:
+        for i, counters in enumerate(PMC_PASSES, 1):
+            cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", os.path.join(d, "p%d" % i), "-o", "run",
+                   "--", *child]
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
+                                 start_new_session=True, cwd=ROOT)
+            try:
+                _, err = p.communicate(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return None, "pmc pass %d (%s) timed out" % (i, " ".join(counters))
+            if p.returncode != 0:
+                return None, "pmc pass %d exited %d: %s" % (i, p.returncode, err.decode(errors="replace")[-300:])
+        return pmc_traffic.summarize(d, [args.batch, args.image_size, args.level, args.mode], verbose=False), \
+            "rocprofv3 --pmc, 3 passes in this run over 3 steps each; FETCH_SIZE/WRITE_SIZE calibrated on a 1 GiB stream"
+    except Exception as e:  # a profiler failure must not lose the bench line
+        return None, "pmc passes failed: %r" % (e,)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def pmc_child(args):
+    """One profiled pass (bench.py --pmc-child under rocprofv3): the workload's steps, then the
+    calibration stream of known byte count."""
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    w = workload(args, 0, dev)
+    for _ in range(args.warmup + args.steps):
+        step(w)
+    torch.cuda.synchronize()
+    copy_ceiling_gbs(dev)
+    torch.cuda.synchronize()
 
 
 def main():
     args = parse()
+    if args.pmc_child:
+        return pmc_child(args)
     world, rank, dev = setup_dist(args)
     w = workload(args, rank, dev)
     for _ in range(args.warmup):
@@ -316,16 +406,31 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     ceiling = copy_ceiling_gbs(dev)
 
-    traffic = valu_busy = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc):
-        try:
-            rec = json.load(open(pmc))
-            if rec.get("config") == [args.batch, args.image_size, args.level, args.mode]:
-                traffic = rec.get("hbm_bytes_per_launch", {}).get(dominant)
-                valu_busy = rec.get("valu_busy", {}).get(dominant)
-        except Exception:
-            traffic = valu_busy = None
+    # HBM traffic and VALU share of the dominant kernel, measured by rocprofv3 --pmc passes in this
+    # run (rank 0 at N = 1, like the CPU baseline)
+    pmc, pmc_note = None, "not measured (N > 1 or --no-pmc)"
+    if world == 1 and rank == 0 and not args.no_pmc:
+        pmc, pmc_note = pmc_passes(args)
+    traffic = valu_busy = valu_insts = wait_share = None
+    if pmc is not None:
+        traffic = pmc.get("hbm_bytes_per_launch", {}).get(dominant)
+        valu_busy = pmc.get("valu_busy", {}).get(dominant)
+        valu_insts = pmc.get("valu_insts", {}).get(dominant)
+        wait_share = pmc.get("wait_any_share", {}).get(dominant)
+    hbm_frac = achieved / HBM_PEAK_GBS
+    valu = None
+    if valu_insts is not None:
+        rate = valu_insts / (dom_ms * 1e-3)
+        valu = {"achieved": round(rate / 1e9, 2), "peak": round(VALU_PEAK_INSTS / 1e9, 1),
+                "unit": "G wave64-VALU instructions/s", "frac": round(rate / VALU_PEAK_INSTS, 5),
+                "busy_share": None if valu_busy is None else round(valu_busy, 4)}
+    # the binding roof is the one the kernel comes closest to; with both well below 1 the kernel is
+    # latency-bound (dependent memory round trips, barriers), which is stated in `limiter`
+    fracs = {"hbm": hbm_frac}
+    if valu is not None:
+        fracs["valu"] = valu["frac"]
+    bound = max(fracs, key=fracs.get)
+    limiter = bound if fracs[bound] >= 0.6 else "latency"
 
     res = {
         "metric": "rasterize Mpixels/s fwd+bwd, 256² batch=64; % HBM roofline at 1 & 8 GPU",
@@ -346,16 +451,18 @@ def main():
                    "global_batch": world * args.batch, "image_size": args.image_size, "faces": w["F"],
                    "channels": w["C"], "parallelism": "batch-sharded dp%d" % world},
         "host_ms_per_step": round(host_elapsed / args.steps * 1e3, 4),
-        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5),
+        "roofline": {"bound": bound, "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(hbm_frac, 5), "traffic": traffic,
+                     "traffic_source": pmc_note, "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5),
                      "copy_ceiling_gbs": round(ceiling, 1),
-                     # the kernel's VALU issue share (PMC pass, tools/pmc_traffic.sh): with the HBM
-                     # share this shows the kernel is bound by neither -- latency
-                     "valu_busy": None if valu_busy is None else round(valu_busy, 3),
-                     # what actually limits the kernel: its HBM share and its
-                     # VALU share are both well below 1, i.e. dependent-load latency and issue
-                     "limiter": "latency"},
+                     # the second roof: VALU issue (SQ_INSTS_VALU over the HIP-event duration)
+                     "valu": valu, "wait_share": None if wait_share is None else round(wait_share, 4),
+                     # what limits the kernel: the closest roof when it is within reach (>= 0.6),
+                     # otherwise latency
+                     "limiter": limiter},
+        "pmc_all_kernels": None if pmc is None else {
+            k: {"traffic": pmc["hbm_bytes_per_launch"].get(k), "valu_busy": round(pmc.get("valu_busy", {}).get(k, 0.0), 4),
+                "wait_share": round(pmc.get("wait_any_share", {}).get(k, 0.0), 4)} for k in pmc["hbm_bytes_per_launch"]},
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "step_roofline_frac": round(total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
     }

@@ -95,8 +95,8 @@ size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins
 // ------------------------------------------------------------------------------------------------
 // device helpers
 
-// rasterize_cuda_kernel.cu:76-77: pixel centre, computed in double, rounded to float
-__device__ __forceinline__ float pix_center(int i, int S) { return (float)((2. * i + 1 - S) / S); }
+// rasterize_cuda_kernel.cu:76-77: pixel centre, (float)((2.0 * i + 1 - S) / S), bit for bit (nr_pixel.h)
+__device__ __forceinline__ float pix_center(int i, int S) { return nr_pixel_centre(i, S); }
 
 // conservative range of pixel indices whose centre may lie in [lo, hi] (float compare).  Empty
 // when lo > hi.  One pixel of margin on each side absorbs the float rounding of the centres.

@@ -55,6 +55,7 @@
 #pragma clang fp contract(off)
 
 #include "nr_cull.h"
+#include "nr_pixel.h"
 #include "nr_common.h"
 #include "nr_shade.h"
 #include "nr_fwd.h"

@@ -249,3 +249,17 @@ def test_tensor_cache_lru():
     assert c.get(kb) is None and c.get(ka) is a and c.get(kd) is d
     a.add_(1)                   # an in-place edit bumps the version: a new key
     assert c.get((a.data_ptr(), a._version)) is None
+
+
+def test_pixel_centre_is_exact_on_host(tmp_path):
+    """csrc/nr_pixel.h (the kernels' pixel centre without doubles: an f32 division, or a 2^-k scaling
+    for a power-of-two raster) equals the reference's (float)((2.0 * i + 1 - S) / S)
+    (rasterize_cuda_kernel.cu:76-77) bit for bit for every i of every raster size up to 16384."""
+    import subprocess
+    exe = str(tmp_path / "pixel_centre_check")
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-I" + os.path.join(ROOT, "neural_renderer_v2_pytorch_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "host", "pixel_centre_check.cpp"), "-o", exe])
+    out = subprocess.run([exe, "16384"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    m = re.match(r"checked (\d+) mismatches (\d+)", out.stdout)
+    assert m and int(m.group(2)) == 0 and int(m.group(1)) > 134000000, out.stdout

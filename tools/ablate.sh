@@ -23,7 +23,7 @@ for r in $(seq 1 ${REPEAT:-1}); do
 i=0
 for V in $VARIANTS; do
   i=$((i+1))
-  NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline > $OUT/bench_${i}_$r.log 2>&1
+  NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --no-pmc > $OUT/bench_${i}_$r.log 2>&1
   rc=$?; echo "$V rc=$rc: $(python -c "import json,sys; d=json.loads(open('$OUT/bench_${i}_$r.log').read().strip().splitlines()[-1]); print(d['kernels_ms'], d['ms_per_step'])")"
   if [ $rc -ne 0 ]; then exit $rc; fi
   if [ -n "$CONFIGS" ]; then

@@ -37,34 +37,9 @@ template <bool LIT> constexpr int srec() { return LIT ? 24 : 20; }
 constexpr int BWD_LDS_IG = 2 * MAXC * HN * 4;
 constexpr int BWD_LDS_HALO = 2 * MAXC * 128 * 4;  // halo staging (step 0), after the I / G planes
 template <bool LIT> constexpr int bwd_lds() {
-#ifdef NR_BWD_LDS_SMALL
-    return BWD_LDS_IG + BWD_LDS_HALO;  // timing builds with NR_ABLATE & 2 only (no record staging)
-#endif
     return BWD_LDS_IG + BWD_LDS_HALO > 4 * 128 * srec<LIT>() * 4 ? BWD_LDS_IG + BWD_LDS_HALO : 4 * 128 * srec<LIT>() * 4;
 }
 static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
-// experiment switch for timing builds (never set in the shipped library):
-//   2 = no gradient accumulation (steps 3 and 4), 4 = no global atomics (step 4),
-//   8 = no per-face gather (step 3's member loop), 16 = no halo shading, 64 = no stencil,
-//   1024 = no direct texel atomics (texels outside a face's window)
-#ifndef NR_ABLATE
-#define NR_ABLATE 0
-#endif
-#ifndef NR_BWD_SKIP_ZERO
-#define NR_BWD_SKIP_ZERO 0  // 1: any all-zero pixel skips the gather (costs the headline ~0.5 %); 0: silhouettes-only renders only
-#endif
-#ifndef NR_BWD_FASTDIV
-#define NR_BWD_FASTDIV 1  // 0: IEEE divisions in the backward's recompute (timing builds)
-#endif
-#ifndef NR_BWD_SKIP_BG
-#define NR_BWD_SKIP_BG 1  // 0: background tiles run the whole kernel (timing builds)
-#endif
-#ifndef NR_HALO_EARLY
-#define NR_HALO_EARLY 1
-#endif
-#ifndef NR_BWD_CHUNK_IL
-#define NR_BWD_CHUNK_IL 1  // lane -> pixel map with 2x2-interleaved gather chunks (0: one pixel row per 16 lanes)
-#endif
 
 // per-wave phase timestamps (timing builds only, tools/bwd_timing.py): lane 0 of every wave of the
 // 2-pixel variant records the shader clock at 8 points of its life
@@ -209,16 +184,14 @@ struct BwdPix {
 };
 
 // FEAT: 1 = lights, 2 = backgrounds, 4 = silhouettes only (separate instantiations keep the plain path lean)
-// NPX: pixels per lane (2: 256 threads, a wave = 16x8 pixels; 1: 512 threads, a wave = 16x4 pixels)
-#ifndef NR_BWD_WPE1
-#define NR_BWD_WPE1 6
-#endif
+// NPX: pixels per lane (2: 256 threads, a wave = 16x8 pixels; 1: 512 threads, a wave = 16x4 pixels,
+// at 6 waves/SIMD)
 // CC: the channel count as a compile-time constant (0: sh.C at run time).  With every channel present
 // (rgb + sil + depth, C = MAXC) the per-channel `c < C` guards of the loads, the LDS staging and the
 // stencil fold away, with their zero defaults and scalar branches; that instantiation is launched
 // only with anti-aliasing and a power-of-two raster (both folded too).
 template <int FEAT, int NPX, int CC = 0>
-__global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? NR_BWD_WPE1 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
+__global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? 6 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
     constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0, SILO = (FEAT & 4) != 0;
     // features this instantiation does not have become compile-time constants (the shared
     // shade_pixel then carries no light / background code or arguments)
@@ -241,13 +214,13 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     const bool want_tex = rgb && a.grad_tex != nullptr;
     constexpr bool wlate = SILO;  // silhouettes only: weights after the stencil, sparse gather
     int b, tile_x, tile_y;
-    block_item_tile<NR_SWZ_MODE, NR_SWZ_W, NR_SWZ_H>(g.group, (S + TW - 1) / TW, (S + BH - 1) / BH, b, tile_x, tile_y);
+    block_item_tile(g.group, (S + TW - 1) / TW, (S + BH - 1) / BH, b, tile_x, tile_y);
     const int tx0 = tile_x * TW;
     const int ty0 = tile_y * BH;
     // a tile with no foreground pixel contributes nothing (every gradient term is per foreground
     // pixel; the halo only feeds foreground pixels' stencils): with the forward's bin flags it ends
     // here.  Backgrounds (BG) get gradient from background pixels, so that instantiation never skips.
-    if (NR_BWD_SKIP_BG && !BG && a.binfg && a.binfg[(long long)b * g.nbins + (ty0 / COARSE) * g.nbx + tx0 / COARSE] == 0) return;
+    if (!BG && a.binfg && a.binfg[(long long)b * g.nbins + (ty0 / COARSE) * g.nbx + tx0 / COARSE] == 0) return;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     const int bt = sh.tv.sb ? b : 0;
@@ -260,7 +233,6 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     float* __restrict__ gtb = a.grad_tex ? a.grad_tex + (long long)bt * 4 * a.HWp : nullptr;
     float* __restrict__ gtpb = a.grad_tex_planar ? a.grad_tex_planar + (long long)bt * 3 * a.HW : nullptr;
     // wave wid owns the 16x8 block at (16 (wid & 1), 8 (wid >> 1)); lane -> (lx, ly0) and (lx, ly0 + 4)
-#if NR_BWD_CHUNK_IL
     // lanes 16 c .. 16 c + 15 (member chunk c of the gather, step 3) hold the pixels of parity class
     // (x & 1, y & 1) = (c & 1, c >> 1) of the wave's region (8 x 2 of them per pixel k, rows 4 apart):
     // a face's pixels split about evenly over the four chunks, so its member loop, which runs as
@@ -268,10 +240,6 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     // the headline: 5.25 instead of 5.95 per face)
     const int lx = (wid & 1) * 16 + 2 * (lane & 7) + ((lane >> 4) & 1);
     const int ly0 = (wid >> 1) * (4 * NPX) + 2 * ((lane >> 3) & 1) + (lane >> 5);
-#else
-    const int lx = (wid & 1) * 16 + (lane & 15);
-    const int ly0 = (wid >> 1) * (4 * NPX) + (lane >> 4);
-#endif
     const int px = tx0 + lx;
     const float xp = pix_center(px, S);
 
@@ -308,9 +276,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         }
     };
     NR_TSTAMP(0);
-#if NR_HALO_EARLY
     halo_prefetch();  // in flight during step 1
-#endif
 
     // ---- 1. image + upstream gradient (LDS), and the stencil-independent gradient terms ---------
     BwdPix P[NPX];
@@ -378,18 +344,12 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         __builtin_amdgcn_sched_barrier(0);  // keeps the scheduler from sinking the uv load to its use
         // the exact shortened divisions (DESIGN.md "Numerics") as in the forward: bit-identical
         // values (v28: bwd 0.284 -> 0.279 ms; before the latency fixes of v27-v28 it measured even)
-        if (!NR_BWD_FASTDIV) f.flags = 0;
-        bool wfast = false;
-        if (NR_ABLATE & 512) {
-            q.w[0] = f.x0, q.w[1] = f.y0, q.w[2] = f.z0;  // timing build: no weights
-        } else {
-            wfast = face_weights(xp, yp, f, q.w);
-        }
+        const bool wfast = face_weights(xp, yp, f, q.w);
         const float* w = q.w;
         float dz[3];  // w_k / z_k, shared by the depth and (FACE_ZQ_EQ faces) the texture sampling
         face_dz(f, w, wfast, dz);
         float r = 0.f, gg = 0.f, bb = 0.f, dep = 0.f;
-        if (rgb && !(NR_ABLATE & 128)) {
+        if (rgb) {
             TexSample s;
             const float uvs[6] = {fuv.a.x, fuv.a.y, fuv.a.z, fuv.a.w, fuv.b.x, fuv.b.y};
             // lights: rgb = texture * cw, so the texture sees G * cw and cw sees G * texture
@@ -471,7 +431,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 #pragma unroll
                         for (int ch = 0; ch < 3; ch++) {
                             const float v = Gt[ch] * s.wt[i];
-                            if (v != 0.f && !(NR_ABLATE & 1024)) unsafeAtomicAdd(gtpb + ch * a.HW + s.idx[i], v);
+                            if (v != 0.f) unsafeAtomicAdd(gtpb + ch * a.HW + s.idx[i], v);
                         }
                     }
                 }
@@ -509,7 +469,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                 q.gz[j] = gzj;
             }
         }
-        if ((sh.draw & NR_DRAW_DEPTH) && !(NR_ABLATE & 256)) {
+        if (sh.draw & NR_DRAW_DEPTH) {
             dep = depth_from_dz(dz, wfast);
             // depth channel gradient: selected from the registers with compile-time indices (a
             // runtime-indexed register array would go to scratch)
@@ -542,9 +502,6 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
         }
     }
-#if !NR_HALO_EARLY
-    halo_prefetch();
-#endif
     // halo ring: image and upstream gradient only
     int hy, hx;
     halo_pixel(t, hy, hx);
@@ -553,10 +510,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     if (a.halo) {
         __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMA halo loads have landed
         // each lane t < NHALO moves the halo values it loaded itself (s_hI/s_hG slot t), so its own
-        // vmcnt wait is enough: no barrier before the move (NR_HALO_BARRIER restores one)
-#ifdef NR_HALO_BARRIER
-        __syncthreads();
-#endif
+        // vmcnt wait is enough: no barrier before the move
         if (t < NHALO) {
             const int hl = hy * HW_ + hx;
 #pragma unroll
@@ -571,7 +525,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         float hI[MAXC], hG[MAXC];
 #pragma unroll
         for (int c = 0; c < MAXC; c++) hI[c] = hG[c] = 0.f;
-        if (!(NR_ABLATE & 16) && h_in) {
+        if (h_in) {
             const int hf = fimb[hpy * S + hpx];
             Face ff;
             FaceUV fu;
@@ -611,19 +565,18 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
             Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
         }
-        const float gx = (NR_ABLATE & 64) ? Im[0] : stencil(a, Im, I0, Ip, Gm, G0, Gp, px, S, C);
+        const float gx = stencil(a, Im, I0, Ip, Gm, G0, Gp, px, S, C);
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
             const bool u = c < C;
             Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
             Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
         }
-        const float gy = (NR_ABLATE & 64) ? Ip[0] : stencil(a, Im, I0, Ip, Gm, G0, Gp, py, S, C);
+        const float gy = stencil(a, Im, I0, Ip, Gm, G0, Gp, py, S, C);
         if (wlate && (gx != 0.f || gy != 0.f)) {
             // silhouettes only: the stencil is zero away from silhouette edges, so only these pixels
             // fetch their face and weights (the same computation as in step 1)
-            Face f = load_face_rec(frb + q.fi * FACE_REC);
-            if (!NR_BWD_FASTDIV) f.flags = 0;
+            const Face f = load_face_rec(frb + q.fi * FACE_REC);
             face_weights(xp, pix_center(py, S), f, q.w);
         }
         // coordinate map: coord = sum_k w_k faces_xy[k]  (rasterize.py:91-97)
@@ -633,13 +586,6 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             gF[k][3 * j + 1] = gy * q.w[j];
             gF[k][3 * j + 2] = q.gz[j];
         }
-    }
-    if (NR_ABLATE & 2) {
-#pragma unroll
-        for (int k = 0; k < NPX; k++)
-#pragma unroll
-            for (int j = 0; j < 9; j++) asm volatile("" ::"v"(gF[k][j]));
-        return;
     }
     NR_TSTAMP(3);
     __syncthreads();  // the staged records reuse the image / gradient LDS
@@ -679,14 +625,12 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     // a pixel whose every contribution is zero stays out of the per-face gather (exact: it would add
     // zeros): silhouettes away from silhouette edges, where the stencil is zero, or any pixel whose
     // upstream gradient is zero (a loss on some channels or regions only)
+    // (testing every pixel for an all-zero record cost the headline ~0.5 %: only silhouettes-only
+    // renders, whose stencil is zero away from silhouette edges, do)
     bool nz[NPX];
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
-        bool v = !NR_BWD_SKIP_ZERO && !wlate;
-        if (NR_BWD_SKIP_ZERO) {
-            v = want_tex && P[k].pos >= 0 && (P[k].grgb[0] != 0.f || P[k].grgb[1] != 0.f || P[k].grgb[2] != 0.f);
-            if (LIT) v = v || P[k].gn[0] != 0.f || P[k].gn[1] != 0.f || P[k].gn[2] != 0.f;
-        }
+        bool v = !wlate;
 #pragma unroll
         for (int j = 0; j < 9; j++) v = v || gF[k][j] != 0.f;
         nz[k] = v;
@@ -719,7 +663,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         p0 &= ~m0;
         p1 &= ~m1;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, af = 0.f, an = 0.f;
-        if (!(NR_ABLATE & 8)) {
+        {
             // this lane's members: those of lanes 16 chunk .. 16 chunk + 15 (parity class `chunk`);
             // bits 0..15 from the first pixel of each lane, 16..31 from the second
             uint32_t mine = ((uint32_t)(m0 >> (16 * chunk)) & 0xffffu) | (((uint32_t)(m1 >> (16 * chunk)) & 0xffffu) << 16);
@@ -766,9 +710,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             if (chunk == 0 && tt < 9 && nt != 0.f) unsafeAtomicAdd(gNb + key * 9 + tt, nt);
         }
         // ---- 4. flush this face: lane (t, c) writes channel c of texel t (c < 3) or face float t (c == 3)
-        if (NR_ABLATE & 4) {
-            asm volatile("" ::"v"(v));
-        } else {
+        {
             // one atomic per lane, address selected without branches: face lanes add this face's
             // floats; texel lanes flush the pending window when the window changes
             const bool win = wx != INT_MIN;
@@ -786,7 +728,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             }
         }
     }
-    if (!(NR_ABLATE & 4)) {  // the last pending window
+    {  // the last pending window
         const int x = pwx + tdx, y = pwy + tdy;
         if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
             unsafeAtomicAdd(gtb + (y * sh.tv.W + x) * 4 + chunk, pend);
@@ -804,27 +746,18 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 // threads, 6 waves/SIMD instead of 4) for small grids, where the waves, not the per-face work, are
 // short (teapot B=4: 0.041 -> 0.035 ms; torus 1024^2 B=1: 0.059 -> 0.048 ms; on the headline and the
 // car the smaller wave regions mean more face flushes: 0.405 -> 0.417 and 0.73 -> 0.84 ms).
-// NR_BWD_NPX: 0 by grid size, 1 / 2 forced (timing builds).
-#ifndef NR_BWD_NPX
-#define NR_BWD_NPX 0
-#endif
-#ifndef NR_BWD_CC
-#define NR_BWD_CC 1  // 0: no compile-time channel count (timing builds)
-#endif
 template <int FEAT>
 void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
-    const bool one = NR_BWD_NPX == 1 || (NR_BWD_NPX == 0 && (long long)grid.x * grid.y < 8192);
+    const bool one = (long long)grid.x * grid.y < 8192;
     if (one)
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
-    else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2 && NR_BWD_CC)
+    else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2)
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC>), grid, dim3(NT), 0, st, ba, g, sh);
     else
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
 }
 
-#ifndef NR_VGRAD_UNROLL
-#define NR_VGRAD_UNROLL 4
-#endif
+constexpr int VGRAD_UNROLL = 4;
 // gathered-face gradient -> vertex gradient: gV[b, v] = sum over (f, k) with faces[f, k] = v of gF[b, f, k]
 // (the index backward of rasterize.py:232), through a CSR adjacency built once per faces tensor.
 __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __restrict__ off,
@@ -841,31 +774,27 @@ __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __res
     const float* base = gF + (long long)b * F * 9;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
     const int e0 = off[v], e1 = off[v + 1];
-#if NR_VGRAD_UNROLL > 1
-    // entries read NR_VGRAD_UNROLL at a time (their row loads in flight together); the sums keep the
+    // entries read VGRAD_UNROLL at a time (their row loads in flight together); the sums keep the
     // CSR order
     int e = e0;
-    for (; e + NR_VGRAD_UNROLL <= e1; e += NR_VGRAD_UNROLL) {
-        int en[NR_VGRAD_UNROLL];
+    for (; e + VGRAD_UNROLL <= e1; e += VGRAD_UNROLL) {
+        int en[VGRAD_UNROLL];
 #pragma unroll
-        for (int u = 0; u < NR_VGRAD_UNROLL; u++) en[u] = ent[e + u];
-        float3 rv[NR_VGRAD_UNROLL];
+        for (int u = 0; u < VGRAD_UNROLL; u++) en[u] = ent[e + u];
+        float3 rv[VGRAD_UNROLL];
 #pragma unroll
-        for (int u = 0; u < NR_VGRAD_UNROLL; u++) {
+        for (int u = 0; u < VGRAD_UNROLL; u++) {
             const float* r = base + (long long)en[u] * 3;
             rv[u] = make_float3(r[0], r[1], r[2]);
         }
 #pragma unroll
-        for (int u = 0; u < NR_VGRAD_UNROLL; u++) {
+        for (int u = 0; u < VGRAD_UNROLL; u++) {
             s0 += rv[u].x;
             s1 += rv[u].y;
             s2 += rv[u].z;
         }
     }
     for (; e < e1; e++) {
-#else
-    for (int e = e0; e < e1; e++) {
-#endif
         const float* r = base + (long long)ent[e] * 3;  // entry = 3 f + k
         s0 += r[0];
         s1 += r[1];

@@ -10,10 +10,9 @@ constexpr int TW = 32;             // tile width  (internal pixels)
 constexpr int TH = 8;              // tile height
 constexpr int NT = TW * TH;        // threads per raster block, one pixel each
 constexpr int COARSE = 32;         // coarse bin edge (pixels) = forward block region; = TW, multiple of TH
-#ifndef NR_SETUP_FACES
-#define NR_SETUP_FACES 192  // 27 blocks per item at 5120 faces: one round of blocks on the chip (128: 0.023 -> 0.020 ms)
-#endif
-constexpr int SETUP_FACES = NR_SETUP_FACES;  // faces per setup block (SETUP_FACES / 32 bitmask words)
+// faces per setup block (SETUP_FACES / 32 bitmask words); 192: 27 blocks per item at 5120 faces, one
+// round of blocks on the chip (128: 0.023 -> 0.020 ms)
+constexpr int SETUP_FACES = 192;
 static_assert(SETUP_FACES % 32 == 0 && SETUP_FACES <= 256, "setup block layout");
 constexpr int SETUP_LDS_WORDS = 12288;  // bin-mask words built in LDS (dynamic LDS, 48 KB: 2048 bins, S <= 1448, at 192 faces)
 // dynamic LDS words of a k_face_setup launch: the staged face records, or the block's mask words of
@@ -95,9 +94,6 @@ size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins
 // ------------------------------------------------------------------------------------------------
 // device helpers
 
-// rasterize_cuda_kernel.cu:76-77: pixel centre, (float)((2.0 * i + 1 - S) / S), bit for bit (nr_pixel.h)
-__device__ __forceinline__ float pix_center(int i, int S) { return nr_pixel_centre(i, S); }
-
 // conservative range of pixel indices whose centre may lie in [lo, hi] (float compare).  Empty
 // when lo > hi.  One pixel of margin on each side absorbs the float rounding of the centres.
 __device__ __forceinline__ void pix_range(float lo, float hi, int S, int& i0, int& i1) {
@@ -178,6 +174,18 @@ __device__ __forceinline__ float div_nr(float a, float b, float r) {
     q = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
     return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
 }
+// rasterize_cuda_kernel.cu:76-77: pixel centre (float)((2.0 * i + 1 - S) / S), bit for bit: the f32
+// division of nr_pixel.h, as the exact shortened sequence (numerator and S are integers of at most 15
+// bits, inside div_nr's exact range; checked for every pixel of every S <= 16384 on the GPU)
+__device__ __forceinline__ float pix_center(int i, int S) {
+    const float s = (float)S;
+    return div_nr((float)(2 * i + 1 - S), s, rcp_nr(s));
+}
+// the same for a wave-uniform i: the value goes to an SGPR (block extents of the forward's walk)
+__device__ __forceinline__ float pix_center_uniform(int i, int S) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(pix_center(i, S))));
+}
+
 // |x| in [2^-e, 2^e]
 __device__ __forceinline__ bool in_range(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }
 // coordinate / depth magnitudes for which the face-level guard below holds: 0 or [2^-20, 2^20]
@@ -339,12 +347,7 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
         const float4* t4b = tv.t4 + (long long)bt * tv.HWp;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-#if defined(NR_ABLATE_TEX) && (NR_ABLATE_TEX & 1)
-            q4[i] = make_float4(s.wt[i], s.x, s.y, 0.f);  // timing build: no texel loads
-            (void)t4b;
-#else
             q4[i] = t4b[s.idx[i]];
-#endif
         }
     } else {
 #pragma unroll
@@ -556,56 +559,18 @@ __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, cons
 // XCD-aware block -> tile map.  Workgroups go round-robin to the 8 XCDs (linear id % 8) and each XCD
 // has its own L2, so with the identity map horizontally adjacent tiles never share a cache, and the
 // halo columns, upstream-gradient lines and face records they have in common are fetched once per
-// XCD.  Two remaps (measured on the headline workload):
-//   mode 1 (groups): runs of SW x SH neighbouring tiles go to one XCD back to back; groups
-//          interleave over the XCDs.  Full tile rows (SW = nx, SH = 1) are the balanced case.
-//   mode 2 (bands):  XCD x takes a band of ny / 8 whole tile rows of each item, the band rotating
-//          with the item so every XCD sees every band over 8 items (balanced over the batch).
-// Both fall back to the identity when the grid does not divide evenly (the linear id of item b
-// starts at b * nx * ny, a multiple of 8 whenever the remap applies).
-#ifndef NR_SWZ_MODE
-#define NR_SWZ_MODE 2
-#endif
-#ifndef NR_SWZ_W
-#define NR_SWZ_W 0  // 0: the full tile row
-#endif
-#ifndef NR_SWZ_H
-#define NR_SWZ_H 1
-#endif
-#ifndef NR_FSWZ_MODE
-#define NR_FSWZ_MODE 2
-#endif
-#ifndef NR_FSWZ_W
-#define NR_FSWZ_W 0
-#endif
-#ifndef NR_SSWZ_MODE
-#define NR_SSWZ_MODE 2  // k_shade: bands of its 1-D block range per XCD (v23: 0.104 -> 0.100 ms on the headline)
-#endif
-#ifndef NR_FSWZ_H
-#define NR_FSWZ_H 1
-#endif
-template <int MODE, int SW_, int SH>
+// XCD.  Bands: XCD x takes a band of ny / 8 whole tile rows of each item, the band rotating with the
+// item so every XCD sees every band over 8 items (balanced over the batch; measured against groups
+// of neighbouring tiles and interleaved full rows in DESIGN.md).  The identity when ny is not a
+// multiple of 8 (the linear id of item b starts at b * nx * ny, a multiple of 8 whenever it applies).
 __device__ __forceinline__ void xcd_tile(int L, int b, int nx, int ny, int& tx, int& ty) {
     tx = L % nx;
     ty = L / nx;
-    if (MODE == 1) {
-        const int SW = SW_ > 0 ? SW_ : nx;
-        const int per = SW * SH;
-        const int ngx = nx / SW;
-        if (per > 1 && nx % SW == 0 && ny % SH == 0 && (ngx * (ny / SH)) % 8 == 0) {
-            const int j = L >> 3, xcd = L & 7;
-            const int grp = (j / per) * 8 + xcd;
-            const int q = j % per;
-            tx = (grp % ngx) * SW + q % SW;
-            ty = (grp / ngx) * SH + q / SW;
-        }
-    } else if (MODE == 2) {
-        if (ny % 8 == 0) {
-            const int j = L >> 3, xcd = L & 7;
-            const int band = (xcd + b) & 7;
-            tx = j % nx;
-            ty = band * (ny >> 3) + j / nx;
-        }
+    if (ny % 8 == 0) {
+        const int j = L >> 3, xcd = L & 7;
+        const int band = (xcd + b) & 7;
+        tx = j % nx;
+        ty = band * (ny >> 3) + j / nx;
     }
 }
 
@@ -619,7 +584,6 @@ __device__ __forceinline__ void xcd_tile(int L, int b, int nx, int ny, int& tx, 
 // foreground bin's waves live ~7x longer than a background bin's).  Smaller groups put fewer items on
 // the same tile at once, which matters to the backward's atomics into a shared texture's hot texels.
 // (group_for picks G on the host.)
-template <int MODE, int SW_, int SH>
 __device__ __forceinline__ void block_item_tile(int G, int nx, int ny, int& b, int& tx, int& ty) {
     if (G > 0) {
         const int L = blockIdx.y * gridDim.x + blockIdx.x;
@@ -632,7 +596,7 @@ __device__ __forceinline__ void block_item_tile(int G, int nx, int ny, int& b, i
         return;
     }
     b = blockIdx.y;
-    xcd_tile<MODE, SW_, SH>(blockIdx.x, b, nx, ny, tx, ty);
+    xcd_tile(blockIdx.x, b, nx, ny, tx, ty);
 }
 // the interleave group for B items and a preferred group size: the preference when it divides B, else
 // all B items; 0 (per-item bands) when B is not a multiple of 8
@@ -640,15 +604,9 @@ inline int group_for(int B, int pref) {
     if (pref <= 0 || B % 8 != 0) return 0;
     return B % pref == 0 ? pref : B;
 }
-#ifndef NR_FWD_GROUP
-#define NR_FWD_GROUP 64
-#endif
-#ifndef NR_BWD_GROUP
-#define NR_BWD_GROUP 64
-#endif
-#ifndef NR_BWD_GROUP_TEX
-#define NR_BWD_GROUP_TEX 16  // a shared texture: fewer items on a tile at once (hot-texel atomics)
-#endif
+constexpr int FWD_GROUP = 64;
+constexpr int BWD_GROUP = 64;
+constexpr int BWD_GROUP_TEX = 16;  // a shared texture: fewer items on a tile at once (hot-texel atomics)
 
 // ------------------------------------------------------------------------------------------------
 // block-wide exclusive scan of one int per thread (NW waves)

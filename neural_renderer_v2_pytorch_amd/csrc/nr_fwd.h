@@ -56,11 +56,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                     fzq = fzq && in_range(c[3 * k + 2] + 1e-10f, 0x1p-20f, 0x1p20f);
                     zeq = zeq && (c[3 * k + 2] + 1e-10f == c[3 * k + 2]);
                 }
-#ifdef NR_NO_FASTDIV
-                const int flags = 0;  // timing build: IEEE divisions everywhere
-#else
                 const int flags = (fxyz ? FACE_FAST_XYZ : 0) | (fzq ? FACE_FAST_ZQ : 0) | (zeq ? FACE_ZQ_EQ : 0);
-#endif
                 float4* rec = reinterpret_cast<float4*>(s_frec + t * FACE_REC);
                 rec[0] = make_float4(c[0], c[1], c[2], c[3]);
                 rec[1] = make_float4(c[4], c[5], c[6], c[7]);
@@ -203,9 +199,10 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //      pixel -- every pixel therefore sees its candidate faces in ascending index order, as the
 //      reference's sequential loop does (.cu:82-149), and the per-pixel state stays in registers
 //      across rounds; the test is split into a per-face pass test and a deferred commit
-//      (NR_FWD_DEFER), and the deep-bin variant first drops faces whose edge tests fail over the
-//      whole 8x8 block (block_culled, NR_FWD_CULL);
-//   shading and the output image are computed by k_shade.
+//      (face_commit), and the deep-bin variant first drops faces whose edge tests fail over the
+//      whole 8x8 block (block_culled);
+//   4. SHADE: the block then shades its bin's 16x16 output pixels (k_shade's work, shade_quad) from
+//      the winners it has just found; otherwise k_shade does it in a launch of its own.
 //   Block sizes (picked per launch, run_face_index): 256 threads = 4 waves, each walking the four 8x8
 //   blocks of a 16x16 quadrant (most per-thread work, least fixed cost per pixel: best when the grid
 //   has many bins of moderate depth, e.g. the headline); 1024 threads = 16 waves, one 8x8 block each
@@ -220,27 +217,21 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //   (x0, x1), (A, C), (B, D), (k2, k0) -- so the compiler evaluates those pairs with packed fp32
 //   instructions (each half rounded as the scalar form) and no register moves.
 constexpr int FREC = 7;  // float4 per staged face
-#ifndef NR_FWD_FCAP256
-#define NR_FWD_FCAP256 160  // staged faces per round of the 256-thread variant (8 blocks per CU need <= 20 KB of LDS; 128 -> 160: headline fwd 0.208 -> 0.195 ms)
-#endif
-#ifndef NR_FWD_FCAP1024
-#define NR_FWD_FCAP1024 512  // ... of the 1024-thread variant (2 blocks per CU: up to 80 KB each; 256 -> 512: car fwd 0.914 -> 0.81 ms, torus 0.151 -> 0.132 ms)
-#endif
+// staged faces per round: 160 for the 256-thread variant (8 blocks per CU need <= 20 KB of LDS;
+// 128 -> 160: headline fwd 0.208 -> 0.195 ms), 512 for the 1024-thread one (2 blocks per CU: up to
+// 80 KB each; 256 -> 512: car fwd 0.914 -> 0.81 ms, torus 0.151 -> 0.132 ms)
 template <int NTF> struct FwdCfg {
+    static_assert(NTF == 256 || NTF == 1024, "forward block sizes");
     static constexpr int NW = NTF / 64;                        // waves
     static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
     static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
-    static constexpr int FCAP = NTF >= 1024 ? NR_FWD_FCAP1024 : NTF >= 512 ? 256 : NR_FWD_FCAP256;  // faces staged per round
+    static constexpr int FCAP = NTF >= 1024 ? 512 : 160;       // faces staged per round
     static constexpr int LDS = FCAP * FREC * 16 + CAND * 4;
-    static_assert(NSUB == 1 || NSUB == 2 || NSUB == 4, "forward block layout");
     // 8x8 block k of wave w: its origin (ox, oy) in the bin
     __device__ static __forceinline__ void block_of(int w, int k, int& ox, int& oy) {
         if (NSUB == 1) {         // 16 waves: wave w owns block (w & 3, w >> 2)
             ox = (w & 3) * 8;
             oy = (w >> 2) * 8;
-        } else if (NSUB == 2) {  // 8 waves: a vertical pair of blocks in quadrant w >> 1
-            ox = ((w >> 1) & 1) * 16 + (w & 1) * 8;
-            oy = (w >> 2) * 16 + k * 8;
         } else {                 // 4 waves: the 16x16 quadrant w, walked as four 8x8 blocks
             ox = (w & 1) * 16 + (k & 1) * 8;
             oy = (w >> 1) * 16 + (k >> 1) * 8;
@@ -248,148 +239,46 @@ template <int NTF> struct FwdCfg {
     }
 };
 
-// the reference's per-face test sequence (.cu:94-148) for one staged face at one pixel; q0, q1 are
-// the record's first two float4 (loaded ahead by the caller); FST = the SoA stride (FCAP)
-// NR_FWD_EAGER: how many of the record's float4 rows the walk loads before the first test (2: the
-// tests load the rest as they go; 6: one LDS round trip for the depth, box and edge tests; 8: all)
-#ifndef NR_FWD_EAGER
-#define NR_FWD_EAGER 5  // the pass test's rows (8-row layout: 2 -> 6 eager rows took the headline forward 0.268 -> 0.259 ms, the car 1.20 -> 1.14 ms)
-#endif
+// The staged record rows of one walked face: the pass test's rows 0-4 are loaded together, before the
+// first test (one LDS round trip; with the loads sunk into the test stages each stage waited for its
+// own: 2 -> 6 eager rows of the earlier 8-row layout took the headline forward 0.268 -> 0.259 ms, the
+// car 1.20 -> 1.14 ms).  FST = the SoA stride (FCAP).
+constexpr int FWD_EAGER = 5;
 template <int FST>
 struct FaceRows {
     float4 r[FREC];
     __device__ __forceinline__ void load(const float4* e) {
 #pragma unroll
-        for (int i = 0; i < NR_FWD_EAGER; i++) r[i] = e[i * FST];
+        for (int i = 0; i < FWD_EAGER; i++) r[i] = e[i * FST];
         // an empty asm that takes the rows keeps the compiler from sinking each load into the branch
         // that first uses it (which costs an LDS round trip per test stage)
 #pragma unroll
-        for (int i = 0; i < NR_FWD_EAGER; i++) asm volatile("" ::"v"(r[i].x), "v"(r[i].y), "v"(r[i].z), "v"(r[i].w));
+        for (int i = 0; i < FWD_EAGER; i++) asm volatile("" ::"v"(r[i].x), "v"(r[i].y), "v"(r[i].z), "v"(r[i].w));
     }
-    __device__ __forceinline__ float4 get(const float4* e, int i) const { return i < NR_FWD_EAGER ? r[i] : e[i * FST]; }
+    __device__ __forceinline__ float4 get(const float4* e, int i) const { return i < FWD_EAGER ? r[i] : e[i * FST]; }
 };
-template <int FST>
-__device__ __forceinline__ void face_test(const float4* e, const FaceRows<FST>& fr, float xp, float yp, float near, float far,
-                                          float delta, float& depth_min, int& best) {
-    const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1);
-#if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 1
-    best += (int)q0.x;  // timing build: no per-pixel test
-    return;
-#endif
-    // The rejections of .cu:94-126 are independent of each other (none changes the state), so their
-    // order is free: the depth-bound reject .cu:124-126 goes first, as it is the cheapest and lets a
-    // whole wave skip a face hidden behind what its pixels already hold.
-    const float4 q3 = fr.get(e, 3);
-    if (depth_min < q3.x) return;
-    // .cu:94-97 (min/max form, exact for non-NaN faces)
-    if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return;
-    const float4 q2 = fr.get(e, 2), q4 = fr.get(e, 4);
-    const float x0 = q1.z, y0 = q1.x, x1 = q1.w, y1 = q1.y, x2 = q3.z, y2 = q3.y;
-    const float A = q2.x, B = q2.z, C = q2.y, D = q2.w, E = q3.w, F = q4.x;
-    // .cu:107-116
-    const float c1 = (yp - y0) * A - B * (xp - x0);
-    const float c2 = (yp - y1) * C - D * (xp - x1);
-    if (c1 * c2 < 0) return;
-    const float c3 = (yp - y2) * E - F * (xp - x2);
-    if (c2 * c3 < 0) return;
-    const float4 q5 = fr.get(e, 5), q6 = fr.get(e, 6);
-#if defined(NR_ABLATE_FWD) && NR_ABLATE_FWD == 2
-    best = __float_as_int(q5.w);  // timing build: no division block
-    return;
-#endif
-    const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
-    // .cu:130-139
-    float w0 = (yp * C - xp * D) + q4.w;
-    float w1 = (yp * E - xp * F) + q4.y;
-    float w2 = (yp * A - xp * B) + q4.z;
-    const float ws = w0 + w1 + w2;
-    float zp;
-    if (__float_as_int(q6.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {
-        // face coordinates and depths within [2^-20, 2^20] (or 0) bound every operand below inside
-        // div_nr's exact range (DESIGN.md "Numerics"); 1/z is staged per face
-        const float rs = rcp_nr(ws);
-        w0 = div_nr(w0, ws, rs);
-        w1 = div_nr(w1, ws, rs);
-        w2 = div_nr(w2, ws, rs);
-        const float sum = div_nr(w0, z0, q6.x) + div_nr(w1, z1, q6.y) + div_nr(w2, z2, q6.z);
-        if (in_range(sum, 0x1p-90f, 0x1p90f)) {
-            const float r = rcp_nr(sum);
-            zp = __builtin_fmaf(__builtin_fmaf(-sum, r, 1.f), r, r);  // div_nr(1, sum, r): 1 * r == r
-            zp = __builtin_fmaf(__builtin_fmaf(-sum, zp, 1.f), r, zp);
-        } else {
-            zp = 1.f / sum;
-        }
-    } else {
-        w0 /= ws;
-        w1 /= ws;
-        w2 /= ws;
-        zp = 1.f / (w0 / z0 + w1 / z1 + w2 / z2);
-    }
-    if (zp <= near || far <= zp) return;
-    if (zp <= depth_min - delta) {  // .cu:145-148
-        depth_min = zp;
-        best = __float_as_int(q5.w);
-    }
-}
-
-// The deferred form of face_test (NR_FWD_DEFER): the walk runs only the state-independent part of
-// the test per face (face_pass), and keeps per pixel the one face that passed it and is not yet
-// committed; the rest of the test -- depth reject, barycentric division chain, near / far and the
-// z-test (face_commit) -- runs for all pending pixels of the wave at once, when a newly walked face
-// passes at a pixel that already has a pending face, and at the end of the block's walk. Every pixel
-// still commits its faces in ascending order with the state the sequential loop has at that point
-// (what was pending has been committed before), so the result is that of .cu:82-149; the division
-// chain, run by the whole wave for any one passing lane, runs about a third as often on the headline.
-#ifndef NR_FWD_DEFER
-#define NR_FWD_DEFER 1
-#endif
-#ifndef NR_FWD_COMMIT_EAGER
-#define NR_FWD_COMMIT_EAGER 1
-#endif
-#ifndef NR_FWD_PASS_UNI
-#define NR_FWD_PASS_UNI 1  // the walk keeps the pass test's outcome as a wave mask (0: face_pass per lane)
-#endif
-#ifndef NR_FWD_PASS_BRANCHLESS
-#define NR_FWD_PASS_BRANCHLESS 1  // edge tests without branches (car fwd 0.849 -> 0.838 ms; headline even)
-#endif
-#ifndef NR_FWD_DYN
-#define NR_FWD_DYN NR_FWD_DEFER  // single-round bins deal their 8x8 blocks out to the waves (k_raster_fwd)
-#endif
-// .cu:94-116, with the depth reject of .cu:124-126 against depth_bound >= the pixel's current
-// minimum (a face it rejects the exact test rejects too); rows 0-5 of the record
-template <int FST>
-__device__ __forceinline__ bool face_pass(const float4* e, const FaceRows<FST>& fr, float xp, float yp, float depth_bound) {
-    const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1), q3 = fr.get(e, 3);
-    if (depth_bound < q3.x) return false;
-    if (xp < q0.x || xp > q0.y || yp < q0.z || yp > q0.w) return false;
-    const float4 q2 = fr.get(e, 2), q4 = fr.get(e, 4);
-    const float c1 = (yp - q1.x) * q2.x - q2.z * (xp - q1.z);  // (yp - y0) A - B (xp - x0)
-    const float c2 = (yp - q1.y) * q2.y - q2.w * (xp - q1.w);  // (yp - y1) C - D (xp - x1)
-    const float c3 = (yp - q3.y) * q3.w - q4.x * (xp - q3.z);  // (yp - y2) E - F (xp - x2)
-#if NR_FWD_PASS_BRANCHLESS
-    return !(c1 * c2 < 0) && !(c2 * c3 < 0);
-#else
-    if (c1 * c2 < 0) return false;
-    return !(c2 * c3 < 0);
-#endif
-}
-// .cu:124-148 for a face that passed face_pass at this pixel (slot: its staging slot, per lane);
+// The reference's per-face test sequence (.cu:94-148) in deferred form: the walk runs only the
+// state-independent part of the test per face (the pass test: .cu:94-116, with the depth reject of
+// .cu:124-126 against a bound >= the pixel's current minimum, so a face it rejects the exact test
+// rejects too), and keeps per pixel the one face that passed it and is not yet committed; the rest of
+// the test -- depth reject, barycentric division chain, near / far and the z-test (face_commit) -- runs
+// for all pending pixels of the wave at once, when a newly walked face passes at a pixel that already
+// has a pending face, and at the end of the block's walk. Every pixel still commits its faces in
+// ascending order with the state the sequential loop has at that point (what was pending has been
+// committed before), so the result is that of .cu:82-149; the division chain, run by the whole wave
+// for any one passing lane, runs about a third as often on the headline.
+// .cu:124-148 for a face that passed the pass test at this pixel (slot: its staging slot, per lane);
 // the winner is recorded as its face id, or (SLOT) as its staging slot
 template <int FST, bool SLOT>
 __device__ __forceinline__ void face_commit(const float4* s_face, int slot, float xp, float yp, float near, float far,
                                             float delta, float& depth_min, int& best) {
     const float4* e = s_face + slot;
     const float4 q3 = e[3 * FST];
-#if NR_FWD_COMMIT_EAGER
     // every row in one LDS round trip (the depth reject would otherwise wait for row 3 first)
     const float4 q2 = e[2 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
     asm volatile("" ::"v"(q2.x), "v"(q2.y), "v"(q2.z), "v"(q2.w), "v"(q3.y), "v"(q3.w), "v"(q4.x), "v"(q4.y));
     asm volatile("" ::"v"(q4.z), "v"(q4.w), "v"(q5.x), "v"(q5.y), "v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w));
     if (depth_min < q3.x) return;
-#else
-    if (depth_min < q3.x) return;
-    const float4 q2 = e[2 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
-#endif
     const float A = q2.x, B = q2.z, C = q2.y, D = q2.w, E = q3.w, F = q4.x;
     const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
     float w0 = (yp * C - xp * D) + q4.w;
@@ -423,11 +312,8 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
     }
 }
 
-// Edge cull of a staged face against an 8x8 block (NR_FWD_CULL, deep-bin variant): true only when
-// the reference's edge tests (.cu:107-116) fail at every pixel centre of the block (nr_cull.h)
-#ifndef NR_FWD_CULL
-#define NR_FWD_CULL 1
-#endif
+// Edge cull of a staged face against an 8x8 block (deep-bin variant): true only when the reference's
+// edge tests (.cu:107-116) fail at every pixel centre of the block (nr_cull.h)
 template <int FST>
 __device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc, float hx, float hy) {
     const float4 q1 = e[1 * FST], q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST];
@@ -441,10 +327,8 @@ template <int FST, bool CULL, bool SLOT>
 __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, int n, int lane, float xp, float yp,
                                            float xc0, float xc1, float yc0, float yc1, float near, float far,
                                            float delta, float& depth_min, int& best) {
-#if NR_FWD_DEFER
     int pend = -1;               // staging slot of my pixel's pending face
     unsigned long long occ = 0;  // the wave's pixels with a pending face
-#endif
     for (int c0 = 0; c0 < n; c0 += 64) {
         bool hit = false;
         if (c0 + lane < n) {
@@ -460,8 +344,7 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
             const float4* e = s_face + slot;
             FaceRows<FST> fr;
             fr.load(e);
-#if NR_FWD_DEFER && NR_FWD_PASS_UNI
-            // face_pass with its outcome kept as a wave mask: the depth and bbox tests of every lane
+            // the pass test with its outcome kept as a wave mask: the depth and bbox tests of every lane
             // form one mask, the edge tests run only when a lane is left (a uniform branch), and the
             // pending slot is set from the mask directly (no per-lane boolean to rebuild a ballot from)
             const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1), q3 = fr.get(e, 3);
@@ -486,25 +369,9 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
                 asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(pend) : "v"(pend), "v"(sv), "s"(cov));
             }
             occ |= cov;
-#elif NR_FWD_DEFER
-            const bool pass = face_pass<FST>(e, fr, xp, yp, depth_min);
-            const unsigned long long cov = __ballot(pass);
-            if (cov & occ) {  // commit first where this face would queue behind a pending one
-                if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
-                pend = -1;
-                occ = 0;
-            }
-            if (pass) pend = slot;
-            occ |= cov;
-#else
-            static_assert(!SLOT, "slot-recording walks need NR_FWD_DEFER");
-            face_test<FST>(e, fr, xp, yp, near, far, delta, depth_min, best);
-#endif
         }
     }
-#if NR_FWD_DEFER
     if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
-#endif
 }
 
 template <int FST>
@@ -540,22 +407,15 @@ __device__ unsigned long long g_fwd_t[NR_FTIMING_MAX];
     } while (0)
 #endif
 
-#ifndef NR_FWD_WPE
-#define NR_FWD_WPE 8
-#endif
-#ifndef NR_FWDS_WPE
-#define NR_FWDS_WPE 8  // 8 waves/SIMD (a few spilled registers in the shading epilogue; 7 waves measured 3 % slower)
-#endif
-#ifndef NR_FWD_FORCE_NT
-#define NR_FWD_FORCE_NT 0  // timing builds: 256 / 512 / 1024 threads for every launch
-#endif
+// 8 waves/SIMD (at v37 7 waves, with no spilled register, measured the same)
+constexpr int FWD_WPE = 8;
 // SHADE (NTF == 256, anti-aliasing, no lights / backgrounds): the block also shades its bin's 16x16
 // output pixels (k_shade's work, shade_quad) from the face ids it has just found, so the face-index
 // map is not read back and k_shade has no launch of its own.
 // CC (SHADE only): the channel count as a compile-time constant; CC = MAXC means rgb + sil + depth,
 // so the epilogue's draw-flag tests and per-channel guards fold away (0: sh.C / sh.draw at run time)
 template <int NTF, bool SHADE, int CC = 0>
-__global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_FWDS_WPE : NR_FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
+__global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
                                                   int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
@@ -563,7 +423,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
-    constexpr bool CULL = NR_FWD_CULL && NTF >= 512;  // deep bins: small faces over each 8x8 block
+    constexpr bool CULL = NTF == 1024;  // deep bins: small faces over each 8x8 block
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
     __shared__ int s_scan[C::NW];
     __shared__ int s_next;  // (dyn) next 8x8 block to walk
@@ -572,7 +432,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
 
     const int S = g.S;
     int b, bin_x, bin_y;
-    block_item_tile<NR_FSWZ_MODE, NR_FSWZ_W, NR_FSWZ_H>(g.group, g.nbx, g.nby, b, bin_x, bin_y);
+    block_item_tile(g.group, g.nbx, g.nby, b, bin_x, bin_y);
     const int bin = bin_y * g.nbx + bin_x;
     const int bx0 = bin_x * COARSE;
     const int by0 = bin_y * COARSE;
@@ -597,7 +457,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
     // instead of idling at the block's end (static quadrants keep 80 % of the waves' time busy on the
     // headline, dealt blocks ~92 %, CPU-counted; measured fwd 0.212 -> 0.208 ms)
     // (not with 16 waves: one block each already; measured 0.824 -> 0.918 ms on the car)
-    const bool dyn = NR_FWD_DYN && NTF < 1024 && g.nwords <= NTF && total0 <= FCAP;
+    const bool dyn = NTF < 1024 && g.nwords <= NTF && total0 <= FCAP;
     int ncand = 0;  // the bin's candidate faces (block-uniform)
     unsigned short* s_slot = reinterpret_cast<unsigned short*>(s_cand);  // (dyn, SHADE) winners' staging slots
     static_assert(!SHADE || CAND * 4 >= COARSE * COARSE * 2, "slot map in the candidate list's space");
@@ -633,9 +493,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
                 float depth_min = far;
                 int best = -1;
                 walk_block<FCAP, CULL, SHADE>(s_face, ncand, lane, pix_center(bx0 + ox + (lane & 7), S),
-                                              pix_center(by0 + oy + (lane >> 3), S), pix_center(bx0 + ox, S),
-                                              pix_center(bx0 + ox + 7, S), pix_center(by0 + oy, S),
-                                              pix_center(by0 + oy + 7, S), near, far, delta, depth_min, best);
+                                              pix_center(by0 + oy + (lane >> 3), S), pix_center_uniform(bx0 + ox, S),
+                                              pix_center_uniform(bx0 + ox + 7, S), pix_center_uniform(by0 + oy, S),
+                                              pix_center_uniform(by0 + oy + 7, S), near, far, delta, depth_min, best);
                 int id = best;
                 if (SHADE) {  // best is the staging slot: its face id is in the record's row 5
                     id = best >= 0 ? __float_as_int(s_face[5 * FCAP + best].w) : -1;
@@ -656,10 +516,10 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(SHADE ? NR_
         for (int k = 0; k < NSUB; k++) {
             int ox, oy;
             C::block_of(wid, k, ox, oy);
-            xcl[k] = pix_center(bx0 + ox, S);
-            xch[k] = pix_center(bx0 + ox + 7, S);
-            ycl[k] = pix_center(by0 + oy, S);
-            ych[k] = pix_center(by0 + oy + 7, S);
+            xcl[k] = pix_center_uniform(bx0 + ox, S);
+            xch[k] = pix_center_uniform(bx0 + ox + 7, S);
+            ycl[k] = pix_center_uniform(by0 + oy, S);
+            ych[k] = pix_center_uniform(by0 + oy + 7, S);
             xp[k] = pix_center(bx0 + ox + (lane & 7), S);
             yp[k] = pix_center(by0 + oy + (lane >> 3), S);
             depth_min[k] = far;

@@ -39,18 +39,6 @@
 
 #include "nr_raster.h"
 
-#ifndef NR_VGRAD_BLOCK
-#define NR_VGRAD_BLOCK 256
-#endif
-#ifndef NR_FUSE_SHADE
-#define NR_FUSE_SHADE 1  // 0: k_shade always has its own launch (timing builds)
-#endif
-#ifndef NR_FWD_CC
-#define NR_FWD_CC 1  // 0: no compile-time channel count in the fused forward (timing builds)
-#endif
-#ifndef NR_FUSE_SHADE1024
-#define NR_FUSE_SHADE1024 1  // the deep-bin / small-grid 1024-thread variant shades too (threads 0-255)
-#endif
 
 #pragma clang fp contract(off)
 
@@ -97,7 +85,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                           void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images,
                           TexPack pk, ZeroFill zf = ZeroFill{nullptr, 0}) {
     Geom g = make_geom(F, S);
-    g.group = group_for(B, NR_FWD_GROUP);
+    g.group = group_for(B, FWD_GROUP);
     int2* bbox = (int2*)ws;
     uint32_t* mask = (uint32_t*)((char*)ws + ws_bbox_bytes(B, F));
     if (B == 0) return NR_OK;
@@ -144,10 +132,10 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     // backgrounds): the face-index map is not read back, and there is one launch fewer
     const long long blocks = (long long)g.nbins * B;
     const double faces_per_bin = (double)F / g.nbins;
-    const int ntf = NR_FWD_FORCE_NT ? NR_FWD_FORCE_NT : ((blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024);
+    const int ntf = (blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024;
     const Shade sh = ra ? make_shade(ra) : Shade{};
-    const bool fuse = NR_FUSE_SHADE && ra && (ntf == 256 || (NR_FUSE_SHADE1024 && ntf == 1024)) && ra->anti_aliasing &&
-                      sh.nl == 0 && !sh.bg && vertices;
+    // the deep-bin / small-grid 1024-thread variant shades too (its threads 0-255)
+    const bool fuse = ra && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
     // per-bin foreground flags after the halo values (the backward skips background tiles)
     uint8_t* binfg = (ra && ra->halo) ? (uint8_t*)ra->halo + halo_flags_offset_bytes(B, S, sh.C) : nullptr;
     {
@@ -159,7 +147,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         if (fuse && ntf == 1024)
             hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
-        else if (fuse && sh.C == MAXC && NR_FWD_CC)  // rgb + sil + depth: compile-time channels
+        else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
             hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
         else if (fuse)
@@ -167,9 +155,6 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
         else if (ntf == 256)
             hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg);
-        else if (ntf == 512)
-            hipLaunchKernelGGL((k_raster_fwd<512, false>), dim3(g.nbins, B), dim3(512), 0, st, face_records, rs, bbox, mask,
                                F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg);
         else
             hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
@@ -180,7 +165,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     const int s = ra->anti_aliasing ? S / 2 : S;
     {
         ProfScope _p(P_SHADE, st);
-        if (NR_SHADE_PX == 1 || (NR_SHADE_PX == 2 && ((long long)s * s + 255) / 256 * B < 4096)) {
+        if (((long long)s * s + 255) / 256 * B < 4096) {
             const dim3 grid((unsigned)(((long long)s * s + (ra->anti_aliasing ? 63 : 255)) / (ra->anti_aliasing ? 64 : 256)), B);
             switch ((sh.nl ? 1 : 0) | (sh.bg ? 2 : 0)) {
                 case 0: hipLaunchKernelGGL(k_shade_px<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
@@ -333,7 +318,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     hipStream_t st = (hipStream_t)stream;
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
     Geom g = make_geom(a->num_faces, S);
-    g.group = group_for(a->batch_size, rgb && !a->tex_stride_b ? NR_BWD_GROUP_TEX : NR_BWD_GROUP);
+    g.group = group_for(a->batch_size, rgb && !a->tex_stride_b ? BWD_GROUP_TEX : BWD_GROUP);
     const int HW = a->tex_height * a->tex_width;
     const int HWp = (HW + 3) & ~3;
     char* w = (char*)workspace;
@@ -404,7 +389,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     if (rgb) to = TexOut{g4, gpl, grad_textures, HW, HWp, (long long)tex_items * HW};
     // k_vertex_grad's blocks also carry the texture-gradient output when that is a few texels per
     // thread; otherwise (no vertices, or a large texture) it gets a launch of its own
-    constexpr int VB = NR_VGRAD_BLOCK;  // small blocks: more of them in flight for this latency-bound gather
+    constexpr int VB = 256;  // small blocks: more of them in flight for this latency-bound gather
     const long long vgrad_threads = (nv + VB - 1) / VB * VB;
     const bool carry = nv > 0 && to.n <= 8 * vgrad_threads;
     if (nv > 0) {

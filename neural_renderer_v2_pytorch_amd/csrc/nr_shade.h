@@ -146,11 +146,10 @@ __device__ __forceinline__ void shade_quad_empty(const Shade& sh, int b, int S, 
 // internal pixels it covers, merged in rgb/sil/depth order, flipped, and 2x2-averaged with the
 // reference's summation order.  Kept out of the rasteriser so that kernel stays lean (registers,
 // occupancy); costs one extra read of the face-index map.
+// 6 waves/SIMD: up to 80 VGPRs, no spills with the packed-texel path (7: a 2-dword spill, same time)
+constexpr int SHADE_WPE = 6;
 template <int FEAT>  // 1 = lights, 2 = backgrounds, as k_raster_bwd
-#ifndef NR_SHADE_WPE
-#define NR_SHADE_WPE 6  // 6 waves/SIMD: up to 80 VGPRs, no spills with the packed-texel path (7: a 2-dword spill, same time)
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 1 : NR_SHADE_WPE, 8))) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 1 : SHADE_WPE, 8))) void k_shade(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
                                                int F, int S, Shade sh_in, int aa, float* __restrict__ images,
                                                float* __restrict__ halo) {
     Shade sh = sh_in;
@@ -159,7 +158,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
     const int s = aa ? S / 2 : S;
     const int b = blockIdx.y;
     int blk = blockIdx.x, unused;
-    xcd_tile<NR_SSWZ_MODE, 1, 1>(blockIdx.x, b, 1, gridDim.x, unused, blk);
+    xcd_tile(blockIdx.x, b, 1, gridDim.x, unused, blk);
     const int o = blk * blockDim.x + threadIdx.x;
     if (o >= s * s) return;
     const int oi = o / s, oj = o - oi * s;
@@ -202,10 +201,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
 // output pixel.  Every internal pixel on a backward tile border stores itself to the halo cache.
 // Measured: k_shade_px is faster only when the grid is small (teapot B=4: 0.0176 -> 0.0136 ms); on the
 // headline the 2x2-per-thread k_shade wins (0.121 vs 0.164 ms: shading is VALU-bound there, and the
-// per-pixel form repeats the per-thread overheads 4x).  NR_SHADE_PX: 0 never, 1 always, 2 by grid size.
-#ifndef NR_SHADE_PX
-#define NR_SHADE_PX 2
-#endif
+// per-pixel form repeats the per-thread overheads 4x), so it is picked by grid size (run_face_index).
 template <int FEAT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 1 : 8, 8))) void k_shade_px(const float* __restrict__ face_records, const int32_t* __restrict__ fim,
                                                   int F, int S, Shade sh_in, int aa, float* __restrict__ images,

@@ -1088,3 +1088,33 @@ def test_car_renderer_render_batch(oracle_mod, dev):
     close_images(img2, ref, "car Renderer.render images")
     close_grads(pv.grad, pc.grad, "car grad projected vertices")
     close_grads(tx.grad, tc.grad, "car grad textures")
+
+
+def test_pixel_centre_division(dev):
+    """The kernels' pixel centre (nr_common.h pix_center: rcp_nr + div_nr of (2 i + 1 - S) by S) equals
+    the IEEE f32 division bit for bit for every i in -2 .. S + 1 of every raster size S <= 16384; the
+    host check (test_host.py::test_pixel_centre_is_exact_on_host) proves that division equal to the
+    reference's double formula (rasterize_cuda_kernel.cu:76-77).  Through nr_selftest_division, whose
+    fast leg is the same div_nr(a, b, rcp_nr(b))."""
+    from neural_renderer_v2_pytorch_amd import _lib
+    sizes = torch.arange(1, 16385, device=dev)
+    lens = sizes + 4
+    starts = torch.cumsum(lens, 0) - lens
+    total = int(lens.sum())
+    done = 0
+    chunk = 1 << 25
+    S_all = torch.repeat_interleave(sizes, lens)
+    i_all = torch.arange(total, device=dev) - torch.repeat_interleave(starts, lens) - 2
+    while done < total:
+        n = min(chunk, total - done)
+        S = S_all[done:done + n]
+        a = (2 * i_all[done:done + n] + 1 - S).float().contiguous()
+        b = S.float().contiguous()
+        qf, qi = torch.empty_like(a), torch.empty_like(a)
+        _lib.check(_lib.lib().nr_selftest_division(_lib.ptr(a), _lib.ptr(b), _lib.ptr(qf), _lib.ptr(qi), n,
+                                                   _lib.stream_of(a)), "nr_selftest_division")
+        assert torch.equal(qi, a / b)
+        bad = qf.view(torch.int32) != qi.view(torch.int32)
+        assert not bad.any(), (int(bad.sum()), a[bad][:4].tolist(), b[bad][:4].tolist())
+        done += n
+    assert done > 134000000

@@ -1,4 +1,4 @@
-# usage: VARIANTS="base NR_SWZ_W=1,NR_SWZ_H=1 NR_ABLATE=2" bash tools/ablate.sh <tag>
+# usage: VARIANTS="base lib:abl/libnr_old.so NR_FWD_TIMING" bash tools/ablate.sh <tag>
 # builds one library per variant (comma-separated -D defines; "base" = none) and benches each;
 # CONFIGS=cfg2,cfg3,cfg5 also times those configs (tools/bench_configs.py).
 set -o pipefail

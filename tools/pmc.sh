@@ -1,20 +1,15 @@
-# usage: [NR_ABLATE=n] bash tools/pmc.sh <tag>: PMC counter passes (one rocprofv3 run per pass) over a short bench
+# usage: [NR_LIB_PATH=lib.so] bash tools/pmc.sh <tag>: PMC counter passes (one rocprofv3 run per pass) over a short bench
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-pmc}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-if [ -n "$NR_ABLATE" ]; then
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math \
-    -fvisibility=hidden -Iinclude -DNR_ABLATE=$NR_ABLATE neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip -o /tmp/libnr_pmc.so || exit 1
-  export NR_LIB_PATH=/tmp/libnr_pmc.so
-fi
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1
 i=0
 while read -r PASS; do
   [ -z "$PASS" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $PASS --output-format csv -d $OUT/p$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $PASS --output-format csv -d $OUT/p$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pmc > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($PASS) rc=$rc"
   if [ $rc -ge 124 ]; then exit $rc; fi
 done <<'PASSES'

@@ -176,14 +176,22 @@ __device__ __forceinline__ float div_nr(float a, float b, float r) {
 }
 // rasterize_cuda_kernel.cu:76-77: pixel centre (float)((2.0 * i + 1 - S) / S), bit for bit: the f32
 // division of nr_pixel.h, as the exact shortened sequence (numerator and S are integers of at most 15
-// bits, inside div_nr's exact range; checked for every pixel of every S <= 16384 on the GPU)
-__device__ __forceinline__ float pix_center(int i, int S) {
+// bits, inside div_nr's exact range; checked for every pixel of every S <= 16384 on the GPU), or an
+// exact scaling when S is a power of two (measured: headline forward 0.169 -> 0.163 ms against the
+// division alone).  pix_center_div: the division without the branch, where the branch would hold
+// several centres live across it (the forward's static walk: 45 spilled registers)
+__device__ __forceinline__ float pix_center_div(int i, int S) {
     const float s = (float)S;
     return div_nr((float)(2 * i + 1 - S), s, rcp_nr(s));
 }
-// the same for a wave-uniform i: the value goes to an SGPR (block extents of the forward's walk)
-__device__ __forceinline__ float pix_center_uniform(int i, int S) {
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(pix_center(i, S))));
+__device__ __forceinline__ float pix_center(int i, int S) {
+    // a power-of-two S (uniform branch): the quotient is exact, a scaling by 2^-log2(S)
+    if ((S & (S - 1)) == 0) return __builtin_ldexpf((float)(2 * i + 1 - S), -__builtin_ctz((unsigned)S));
+    return pix_center_div(i, S);
+}
+// lane l's value of v, wave-uniform (an SGPR)
+__device__ __forceinline__ float lane_value(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
 // |x| in [2^-e, 2^e]

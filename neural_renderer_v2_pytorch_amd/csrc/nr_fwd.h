@@ -492,10 +492,11 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                 const int ox = (u & 3) * 8, oy = (u >> 2) * 8;
                 float depth_min = far;
                 int best = -1;
-                walk_block<FCAP, CULL, SHADE>(s_face, ncand, lane, pix_center(bx0 + ox + (lane & 7), S),
-                                              pix_center(by0 + oy + (lane >> 3), S), pix_center_uniform(bx0 + ox, S),
-                                              pix_center_uniform(bx0 + ox + 7, S), pix_center_uniform(by0 + oy, S),
-                                              pix_center_uniform(by0 + oy + 7, S), near, far, delta, depth_min, best);
+                // the block's pixel-centre extent: lanes 0 / 7 hold its first / last column, lanes
+                // 0 / 56 its first / last row (read into SGPRs, no recomputation)
+                const float xp = pix_center(bx0 + ox + (lane & 7), S), yp = pix_center(by0 + oy + (lane >> 3), S);
+                walk_block<FCAP, CULL, SHADE>(s_face, ncand, lane, xp, yp, lane_value(xp, 0), lane_value(xp, 7),
+                                              lane_value(yp, 0), lane_value(yp, 56), near, far, delta, depth_min, best);
                 int id = best;
                 if (SHADE) {  // best is the staging slot: its face id is in the record's row 5
                     id = best >= 0 ? __float_as_int(s_face[5 * FCAP + best].w) : -1;
@@ -516,12 +517,12 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         for (int k = 0; k < NSUB; k++) {
             int ox, oy;
             C::block_of(wid, k, ox, oy);
-            xcl[k] = pix_center_uniform(bx0 + ox, S);
-            xch[k] = pix_center_uniform(bx0 + ox + 7, S);
-            ycl[k] = pix_center_uniform(by0 + oy, S);
-            ych[k] = pix_center_uniform(by0 + oy + 7, S);
-            xp[k] = pix_center(bx0 + ox + (lane & 7), S);
-            yp[k] = pix_center(by0 + oy + (lane >> 3), S);
+            xp[k] = pix_center_div(bx0 + ox + (lane & 7), S);
+            yp[k] = pix_center_div(by0 + oy + (lane >> 3), S);
+            xcl[k] = lane_value(xp[k], 0);
+            xch[k] = lane_value(xp[k], 7);
+            ycl[k] = lane_value(yp[k], 0);
+            ych[k] = lane_value(yp[k], 56);
             depth_min[k] = far;
             best[k] = -1;
         }

@@ -209,13 +209,15 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //   (the bin's walks run 4x wider: small batches, where the grid is a few blocks per CU, and dense
 //   bins -- 300+ faces over one 8x8 block on a 50k-face torus -- no longer serialise on 4 waves).
 //   LDS face record, structure of arrays (float4 i of staged face j at s_face[i * FCAP + j]: the
-//   staging stores are lane-contiguous), 7 x float4; the pass test reads rows 0-4, the commit 2-6:
-//     0: xmin xmax ymin ymax | 1: y0 y1 x0 x1 | 2: A=x1-x0 C=x2-x1 B=y1-y0 D=y2-y1 | 3: zmin y2 x2 E=x0-x2
-//     4: F=y0-y2 k1 k2 k0 | 5: z0 z1 z2 id | 6: 1/z0 1/z1 1/z2 ok
-//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit).  The
-//   operands of edges 1 and 2 and of weights 2 and 0 sit in aligned register pairs -- (y0, y1),
-//   (x0, x1), (A, C), (B, D), (k2, k0) -- so the compiler evaluates those pairs with packed fp32
-//   instructions (each half rounded as the scalar form) and no register moves.
+//   staging stores are lane-contiguous), 7 x float4; the pass test reads rows 0-4 (the depth and bbox
+//   tests rows 0-1, issued first), the commit rows 1 and 3-6:
+//     0: xmin xmax ymin ymax | 1: zmin k0 k2 k1 | 2: y0 y2 x0 x2 | 3: A=x1-x0 E=x0-x2 B=y1-y0 F=y0-y2
+//     4: y1 x1 C=x2-x1 D=y2-y1 | 5: z0 z1 z2 id | 6: 1/z0 1/z1 1/z2 ok
+//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit).  Every
+//   pair the edge tests and weights combine sits in an aligned register pair of one row -- (y0, y2),
+//   (x0, x2), (A, E), (B, F), (y1, x1), (C, D), (k2, k1) -- and is evaluated as a two-wide vector
+//   (packed fp32 instructions, each half rounded as the scalar form, no register moves: v38 had 8
+//   moves per walked face).
 constexpr int FREC = 7;  // float4 per staged face
 // staged faces per round: 160 for the 256-thread variant (8 blocks per CU need <= 20 KB of LDS;
 // 128 -> 160: headline fwd 0.208 -> 0.195 ms), 512 for the 1024-thread one (2 blocks per CU: up to
@@ -273,17 +275,19 @@ template <int FST, bool SLOT>
 __device__ __forceinline__ void face_commit(const float4* s_face, int slot, float xp, float yp, float near, float far,
                                             float delta, float& depth_min, int& best) {
     const float4* e = s_face + slot;
-    const float4 q3 = e[3 * FST];
-    // every row in one LDS round trip (the depth reject would otherwise wait for row 3 first)
-    const float4 q2 = e[2 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
-    asm volatile("" ::"v"(q2.x), "v"(q2.y), "v"(q2.z), "v"(q2.w), "v"(q3.y), "v"(q3.w), "v"(q4.x), "v"(q4.y));
-    asm volatile("" ::"v"(q4.z), "v"(q4.w), "v"(q5.x), "v"(q5.y), "v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w));
-    if (depth_min < q3.x) return;
-    const float A = q2.x, B = q2.z, C = q2.y, D = q2.w, E = q3.w, F = q4.x;
+    const float4 q1 = e[1 * FST];
+    // every row in one LDS round trip (the depth reject would otherwise wait for row 1 first)
+    const float4 q3 = e[3 * FST], q4 = e[4 * FST], q5 = e[5 * FST], q6 = e[6 * FST];
+    asm volatile("" ::"v"(q3.x), "v"(q3.y), "v"(q3.z), "v"(q3.w), "v"(q4.z), "v"(q4.w), "v"(q1.y), "v"(q1.z));
+    asm volatile("" ::"v"(q1.w), "v"(q5.x), "v"(q5.y), "v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w));
+    if (depth_min < q1.x) return;
     const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
-    float w0 = (yp * C - xp * D) + q4.w;
-    float w1 = (yp * E - xp * F) + q4.y;
-    float w2 = (yp * A - xp * B) + q4.z;
+    // .cu:130-132 as pairs (each half rounded as the scalar form): (w2, w1) = (yp (A, E) - xp (B, F))
+    // + (k2, k1), w0 = (yp C - xp D) + k0
+    const f32x2 w21 = (f32x2{yp, yp} * f32x2{q3.x, q3.y} - f32x2{xp, xp} * f32x2{q3.z, q3.w}) + f32x2{q1.z, q1.w};
+    const f32x2 t0 = f32x2{yp, xp} * f32x2{q4.z, q4.w};
+    float w0 = (t0.x - t0.y) + q1.y;
+    float w1 = w21.y, w2 = w21.x;
     const float ws = w0 + w1 + w2;
     float zp;
     if (__float_as_int(q6.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {  // as face_test
@@ -316,9 +320,9 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
 // edge tests (.cu:107-116) fail at every pixel centre of the block (nr_cull.h)
 template <int FST>
 __device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc, float hx, float hy) {
-    const float4 q1 = e[1 * FST], q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST];
+    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST];
     // x0 y0 x1 y1 x2 y2 A B C D E F
-    return nr_block_culled(q1.z, q1.x, q1.w, q1.y, q3.z, q3.y, q2.x, q2.z, q2.y, q2.w, q3.w, q4.x, xc, yc, hx, hy);
+    return nr_block_culled(q2.z, q2.x, q4.y, q4.x, q2.w, q2.y, q3.x, q3.z, q4.z, q4.w, q3.y, q3.w, xc, yc, hx, hy);
 }
 
 // one wave's walk of the n staged faces over its 8x8 block (pixel (xp, yp) per lane, pixel-centre
@@ -347,17 +351,23 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
             // the pass test with its outcome kept as a wave mask: the depth and bbox tests of every lane
             // form one mask, the edge tests run only when a lane is left (a uniform branch), and the
             // pending slot is set from the mask directly (no per-lane boolean to rebuild a ballot from)
-            const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1), q3 = fr.get(e, 3);
-            // (bitwise & and |: no short-circuit control flow)
-            const unsigned long long pre = __ballot((!(depth_min < q3.x)) &
-                                                    !((xp < q0.x) | (xp > q0.y) | (yp < q0.z) | (yp > q0.w)));
+            const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1);
+            // each comparison straight to a lane mask (v_cmp into an SGPR pair; the masks combine on the
+            // scalar unit): a ballot of the combined boolean costs a v_cndmask + v_cmp per face to
+            // rebuild the mask.  !(a < b) is "a >= b or unordered" (UGE), !(a > b) is ULE.
+            const unsigned long long pre = lane_mask_uge(depth_min, q1.x) & lane_mask_uge(xp, q0.x) &
+                                           lane_mask_ule(xp, q0.y) & lane_mask_uge(yp, q0.z) & lane_mask_ule(yp, q0.w);
             unsigned long long cov = 0;
             if (pre) {
-                const float4 q2 = fr.get(e, 2), q4 = fr.get(e, 4);
-                const float c1 = (yp - q1.x) * q2.x - q2.z * (xp - q1.z);
-                const float c2 = (yp - q1.y) * q2.y - q2.w * (xp - q1.w);
-                const float c3 = (yp - q3.y) * q3.w - q4.x * (xp - q3.z);
-                cov = __ballot(!((c1 * c2 < 0) | (c2 * c3 < 0))) & pre;
+                // .cu:107-116 as register pairs (rows 1-3 hold each pair's operands side by side, so
+                // no operand moves): (c1, c3) = (yp - (y0, y2)) (A, E) - (B, F) (xp - (x0, x2)),
+                // c2 = (yp - y1) C - D (xp - x1); pass unless c1 c2 < 0 or c2 c3 < 0
+                const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
+                const f32x2 c13 = (f32x2{yp, yp} - f32x2{q2.x, q2.y}) * f32x2{q3.x, q3.y} -
+                                  f32x2{q3.z, q3.w} * (f32x2{xp, xp} - f32x2{q2.z, q2.w});
+                const f32x2 t2 = (f32x2{yp, xp} - f32x2{q4.x, q4.y}) * f32x2{q4.z, q4.w};
+                const f32x2 p = c13 * (t2.x - t2.y);
+                cov = lane_mask_uge(p.x, 0.f) & lane_mask_uge(p.y, 0.f) & pre;
             }
             if (cov & occ) {  // commit first where this face would queue behind a pending one
                 if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
@@ -380,10 +390,10 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
     const float x2 = c[6], y2 = c[7], z2 = c[8];
     e[0 * FST] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
                        fmaxf(fmaxf(y0, y1), y2));
-    e[1 * FST] = make_float4(y0, y1, x0, x1);
-    e[2 * FST] = make_float4(x1 - x0, x2 - x1, y1 - y0, y2 - y1);
-    e[3 * FST] = make_float4(fminf(fminf(z0, z1), z2), y2, x2, x0 - x2);
-    e[4 * FST] = make_float4(y0 - y2, x2 * y0 - x0 * y2, x0 * y1 - x1 * y0, x1 * y2 - x2 * y1);
+    e[1 * FST] = make_float4(fminf(fminf(z0, z1), z2), x1 * y2 - x2 * y1, x0 * y1 - x1 * y0, x2 * y0 - x0 * y2);
+    e[2 * FST] = make_float4(y0, y2, x0, x2);
+    e[3 * FST] = make_float4(x1 - x0, x0 - x2, y1 - y0, y0 - y2);
+    e[4 * FST] = make_float4(y1, x1, x2 - x1, y2 - y1);
     e[5 * FST] = make_float4(z0, z1, z2, __int_as_float(f));
     const bool ok = coord_ok(x0) && coord_ok(y0) && coord_ok(x1) && coord_ok(y1) && coord_ok(x2) && coord_ok(y2) &&
                     in_range(z0, 0x1p-20f, 0x1p20f) && in_range(z1, 0x1p-20f, 0x1p20f) &&

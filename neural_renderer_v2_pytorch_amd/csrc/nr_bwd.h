@@ -530,7 +530,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             Face ff;
             FaceUV fu;
             load_shading_face(sh, frb, b, hf, ff, fu);
-            shade_pixel(sh, b, hf, ff, fu, hpx, hpy, S, hI);
+            shade_pixel(sh, b, hf, ff, fu, hpx, hpy, pix_center(hpx, S), pix_center(hpy, S), S, hI);
             upstream_grad(a, gimb, C, hpy, hpx, S, hG);
         }
         const int hl = hy * HW_ + hx;

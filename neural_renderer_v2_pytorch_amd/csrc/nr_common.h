@@ -528,10 +528,11 @@ __device__ __forceinline__ void load_shading_face(const Shade& sh, const float* 
                          : k_zero_rec);
 }
 
+// (xp, yp): the pixel centre of (x, y) (pix_center), computed by the caller, which often shares them
+// between pixels (shade_quad: two columns and two rows)
 __device__ __forceinline__ void shade_pixel(const Shade& sh, int b, int fi, const Face& f, const FaceUV& fuv, int x, int y,
-                                            int S, float* out) {
+                                            float xp, float yp, int S, float* out) {
     const bool R = (sh.draw & NR_DRAW_RGB) != 0, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;
-    const float xp = pix_center(x, S), yp = pix_center(y, S);
     float r = 0.f, gg = 0.f, bb = 0.f, sil = 0.f, dep = 0.f;
     if (fi >= 0) sil = 1.f;
     // the weights (and the face record) only feed rgb and depth: a silhouettes-only render skips them

@@ -70,13 +70,16 @@ __device__ __forceinline__ void shade_quad(const Shade& sh, const float* __restr
     const int o = ((S - 2 - iy) >> 1) * s + ((S - 2 - ix) >> 1);
     float* ob = images + (long long)b * sh.C * s * s + o;
     const int ys[4] = {iy + 1, iy, iy + 1, iy}, xs[4] = {ix + 1, ix + 1, ix, ix};
+    // the quad's two column and two row centres
+    const float cx0 = pix_center(ix, S), cx1 = pix_center(ix + 1, S), cy0 = pix_center(iy, S), cy1 = pix_center(iy + 1, S);
+    const float xps[4] = {cx1, cx1, cx0, cx0}, yps[4] = {cy1, cy0, cy1, cy0};
     float v[4][MAXC];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         Face f;
         FaceUV u;
         load_shading_face(sh, frb, b, fis[q], f, u);
-        shade_pixel(sh, b, fis[q], f, u, xs[q], ys[q], S, v[q]);
+        shade_pixel(sh, b, fis[q], f, u, xs[q], ys[q], xps[q], yps[q], S, v[q]);
     }
 #pragma unroll
     for (int c = 0; c < MAXC; c++)
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
         FaceUV u;
         load_shading_face(sh, frb, b, fi, f, u);
         float v[MAXC];
-        shade_pixel(sh, b, fi, f, u, x, y, S, v);
+        shade_pixel(sh, b, fi, f, u, x, y, pix_center(x, S), pix_center(y, S), S, v);
 #pragma unroll
         for (int c = 0; c < MAXC; c++)
             if (c < sh.C) ob[c * s * s] = v[c];
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & 1) 
     FaceUV u;
     load_shading_face(sh, frb, b, fi, f, u);
     float v[MAXC];
-    shade_pixel(sh, b, fi, f, u, x, y, S, v);
+    shade_pixel(sh, b, fi, f, u, x, y, pix_center(x, S), pix_center(y, S), S, v);
     const bool live = o < s * s;
     if (halo && live) halo_store(halo, b, sh.C, S, x, y, v);
     float* ob = images + (long long)b * sh.C * s * s + o;

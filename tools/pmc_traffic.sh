@@ -10,7 +10,7 @@ mkdir -p $OUT
 i=0
 for PASS in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $PASS --output-format csv -d $OUT/p$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $PASS --output-format csv -d $OUT/p$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pmc > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($PASS) rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done

@@ -247,12 +247,16 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     // (lane t < NHALO carries halo pixel t, ring order of halo_pixel), landed before the barrier
     float(*s_hI)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4);
     float(*s_hG)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4 + MAXC * 128);
+    // the halo pixel's bin flag: the forward writes no halo values for a bin without candidate faces
+    // (all 0 there); backgrounds (BG) fill such bins with the background colour, and k_shade writes them
+    int h_live = 1;
     auto halo_prefetch = [&]() {
         if (a.halo && t < 128) {
             int hy, hx;
             halo_pixel(t, hy, hx);
             const int hpy = ty0 - 1 + hy, hpx = tx0 - 1 + hx;
             const bool h_in = t < NHALO && hpy >= 0 && hpy < S && hpx >= 0 && hpx < S;
+            if (!BG && a.binfg && h_in) h_live = a.binfg[(long long)b * g.nbins + (hpy / COARSE) * g.nbx + hpx / COARSE];
             int hoff = 0, hcs = 0;
             if (h_in) halo_locate(C, S, hpx, hpy, hoff, hcs);
             // opaque copies of the base pointers: keeps the compiler from sharing these address
@@ -516,7 +520,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 #pragma unroll
             for (int c = 0; c < MAXC; c++) {
                 if (c < C) {
-                    s_I[c][hl] = h_in ? s_hI[c][t] : 0.f;
+                    s_I[c][hl] = h_in && h_live ? s_hI[c][t] : 0.f;
                     s_G[c][hl] = h_in ? (a.aa ? s_hG[c][t] / 4.f : s_hG[c][t]) : 0.f;
                 }
             }

@@ -608,7 +608,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     }
     if (SHADE && ncand == 0) {
         // an empty bin: every channel of its output pixels is 0 (sil, depth and rgb of background;
-        // no backgrounds in this variant), as is every halo value
+        // no backgrounds in this variant), as is every halo value.  With the bin flags the halo values
+        // are not written: the backward reads a halo pixel of a flagged-empty bin as 0
         Shade sh = sh_in;
         if (CC == MAXC) {
             sh.C = MAXC;
@@ -616,7 +617,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         }
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
-        if ((NTF == 256 || t < 256) && iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, halo);
+        if ((NTF == 256 || t < 256) && iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, binfg ? nullptr : halo);
         NR_FTSTAMP(4, clock64());
         NR_FTSTAMP(5, clock64());
         NR_FTSTAMP(6, 0ull);

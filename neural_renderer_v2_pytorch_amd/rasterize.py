@@ -303,6 +303,9 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj
 # the forward stores the backward's tile-border image values (NrRasterArgs.halo); False makes the
 # backward re-shade its halos instead (same results; the parity tests cover both)
 _HALO_CACHE = os.environ.get("NR_HALO_CACHE", "1") != "0"
+# test hook: a value the halo cache is filled with before the forward (NaN in the parity tests, which
+# so check that the backward reads only values the forward wrote, or infers from the bin flags)
+_HALO_FILL = None
 # the forward packs the texels into RGBA rows that forward and backward sample (NrRasterArgs.
 # textures_packed); False samples the [B, 3, H, W] textures directly (same results)
 _TEX_PACK = os.environ.get("NR_TEX_PACK", "1") != "0"
@@ -354,6 +357,8 @@ class Rasterize(torch.autograd.Function):
         if _HALO_CACHE and any(ctx.needs_input_grad[:2]):
             halo = torch.empty(L.nr_halo_bytes(B, cfg.image_size, int(cfg.aa), cfg.flags) // 4, dtype=torch.float32,
                                device=dev)
+            if _HALO_FILL is not None:
+                halo.fill_(_HALO_FILL)
         light = None
         if light_recs is not None:
             nadj = _normal_adjacency(faces, cfg.V)

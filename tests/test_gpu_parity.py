@@ -589,7 +589,9 @@ def test_exact_division_shortcut(dev):
 @pytest.mark.parametrize("aa,size,extras", [(True, 64, False), (False, 70, False), (True, 48, True)])
 def test_halo_cache_matches_reshading(dev, aa, size, extras):
     """The backward's tile halos read from the forward's halo cache give the same gradients as
-    re-shading them (NrRasterArgs.halo NULL); includes a size that is not a multiple of the tiles."""
+    re-shading them (NrRasterArgs.halo NULL); includes a size that is not a multiple of the tiles.
+    The cache starts out as NaN: the forward writes no halo values for a bin without candidate faces,
+    and the backward must read those as 0 (from the bin flags) and never an unwritten value."""
     B = 3
     proj, f = _ico_batch(3, B, dev)
     vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
@@ -598,6 +600,7 @@ def test_halo_cache_matches_reshading(dev, aa, size, extras):
     grads = []
     for use in (True, False):
         nrr._HALO_CACHE = use
+        nrr._HALO_FILL = float("nan")
         try:
             pv = proj.to(dev).requires_grad_(True)
             tx = tex.clone().requires_grad_(True)
@@ -616,7 +619,9 @@ def test_halo_cache_matches_reshading(dev, aa, size, extras):
             grads.append((img.detach(), pv.grad, tx.grad))
         finally:
             nrr._HALO_CACHE = True
+            nrr._HALO_FILL = None
     assert torch.equal(grads[0][0], grads[1][0])
+    assert torch.isfinite(grads[0][1]).all() and torch.isfinite(grads[0][2]).all()
     close_grads(grads[0][1], grads[1][1], "grad vertices")
     close_grads(grads[0][2], grads[1][2], "grad textures")
 

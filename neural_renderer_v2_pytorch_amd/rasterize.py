@@ -314,7 +314,9 @@ _TEX_PACK = os.environ.get("NR_TEX_PACK", "1") != "0"
 _BWD_PREZERO = os.environ.get("NR_BWD_PREZERO", "1") != "0"
 # only small workspaces: there the separate zero fill is a latency-bound launch (headline: 12 MB,
 # step 0.516 -> 0.505 ms); a large one is bandwidth-bound either way and only lengthens the setup
-# (the car with its atlas gradient: 63 MB, setup 0.052 -> 0.063 ms, step no better)
+# (the car with its atlas gradient: 63 MB, setup 0.052 -> 0.063 ms, step no better).  The cost: a
+# grad-enabled forward whose backward never runs (a render kept for logging, validation without
+# no_grad) still allocates and zero-fills the workspace, and holds it as long as its graph lives.
 _BWD_PREZERO_MAX = 32 << 20
 _TEX_PACK_MAX_BYTES = 1 << 31
 

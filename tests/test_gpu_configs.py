@@ -275,13 +275,17 @@ def test_fwd256_wide_bin_masks_vs_oracle(oracle_mod, dev):
         close_grads(pv.grad[i:i + 1], rgv[k:k + 1], "item %d grad vertices" % i)
 
 
-def test_bin_border_faces_background_skip(oracle_mod, dev):
+@pytest.mark.parametrize("aa", [False, True])
+def test_bin_border_faces_background_skip(oracle_mod, dev, aa):
     """The backward skips a 32x16 tile whose 32x32 bin has no candidate face and reads foreground
     pixels' neighbour values from the halo cache.  Small triangles hug the right and bottom borders
     of every other bin (a checkerboard; the rest are empty), their edges at -1.5 ... +1.5 px from
-    the border, B = 2, 256^2 without anti-aliasing, textured rgb + sil + depth: gradients with the
-    halo cache (skip active) and without (every tile recomputed), and both against the oracle."""
+    the border, B = 2, a 256^2 raster (without anti-aliasing, or the 128^2 anti-aliased output, whose
+    fused forward writes no halo values for the empty bins), textured rgb + sil + depth: gradients
+    with the halo cache (skip active; the cache NaN-filled first) and without (every tile
+    recomputed), and both against the oracle."""
     S, B = 256, 2
+    s = S // 2 if aa else S
     r = np.random.RandomState(49)
     offs = [-1.5, -1.0, -0.5, -0.01, 0.0, 0.01, 0.5, 1.0, 1.5]
     tris = []
@@ -304,21 +308,23 @@ def test_bin_border_faces_background_skip(oracle_mod, dev):
         verts[b, :, 2] = z.reshape(-1)
     f = np.arange(F * 3, dtype=np.int32).reshape(F, 3)
     proj = torch.as_tensor(verts)
-    g = torch.randn((B, 5, S, S), generator=torch.Generator().manual_seed(50))
+    g = torch.randn((B, 5, s, s), generator=torch.Generator().manual_seed(50))
     out = {}
     for halo in (True, False):
         nrr._HALO_CACHE = halo
+        nrr._HALO_FILL = float("nan")  # no unwritten halo value may reach a gradient
         try:
             params, tex, tex_cpu, vt, ft = _textured(F, B, dev, 51)
             pv = proj.to(dev).requires_grad_(True)
             img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params,
-                                          nr.RasterizeHyperparam(image_size=S, anti_aliasing=False), return_face_index=True)
+                                          nr.RasterizeHyperparam(image_size=s, anti_aliasing=aa), return_face_index=True)
             img.backward(g.to(dev))
             out[halo] = (img.detach(), fim, pv.grad, tex.grad)
         finally:
             nrr._HALO_CACHE = True
+            nrr._HALO_FILL = None
     assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
-    ref, rfim, rgv, rgt = _oracle(oracle_mod, proj, f, range(B), S, g, tex_cpu, vt, ft, anti_aliasing=False)
+    ref, rfim, rgv, rgt = _oracle(oracle_mod, proj, f, range(B), s, g, tex_cpu, vt, ft, anti_aliasing=aa)
     assert np.array_equal(out[True][1].cpu().numpy(), rfim)
     assert int((rfim >= 0).sum()) > 2000
     for halo in (True, False):

@@ -440,16 +440,13 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                     }
                 }
             }
-            // texture coordinates -> z (gradient-only terms: reciprocal multiplies)
-            const float ayv = q.ay, byv = q.by, axv = q.ax, bxv = q.bx;
-            float g_x = -(gw[0] * ayv);
-            g_x = g_x + gw[1] * ayv;
-            g_x = g_x - gw[2] * byv;
-            g_x = g_x + gw[3] * byv;
-            float g_y = -(gw[0] * axv);
-            g_y = g_y - gw[1] * bxv;
-            g_y = g_y + gw[2] * axv;
-            g_y = g_y + gw[3] * bxv;
+            // texture coordinates -> z.  Gradient-only terms (within the gradient tolerance, they feed
+            // no comparison): fused multiply-adds, factored sums, and the face record's reciprocals
+            // 1 / (z_k + 1e-10) in place of a v_rcp each.
+            //   d pr_q / d zq_k = -dt w_k uv_kq / zq_k^2, d dt / d zq_k = dt^2 w_k / zq_k^2, so
+            //   d/dzq_k = w_k / zq_k^2 (dt^2 g_dt - dt (gpr_0 u_k + gpr_1 v_k))
+            const float g_x = __builtin_fmaf(gw[1] - gw[0], q.ay, (gw[3] - gw[2]) * q.by);
+            const float g_y = __builtin_fmaf(gw[2] - gw[0], q.ax, (gw[3] - gw[1]) * q.bx);
             const float gp[2] = {g_x, g_y};
             float gpr[2];
 #pragma unroll
@@ -459,18 +456,14 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                 float gq = gp[j];
                 gq = (pc == hm) ? gq * 0.5f : (pc > hm ? 0.f : gq);
                 gq = (pr == lo) ? gq * 0.5f : (pr < lo ? 0.f : gq);
-                gpr[j] = gq;
+                gpr[j] = gq * s.dt;
             }
-            const float g_dt = gpr[0] * s.num[0] + gpr[1] * s.num[1];
-            const float g_st = -g_dt * (s.dt * s.dt);
+            const float g_dt = __builtin_fmaf(gpr[0], s.num[0], gpr[1] * s.num[1]);  // dt g_dt
+            const float rq[3] = {f.rq0, f.rq1, f.rq2};
 #pragma unroll
             for (int j = 0; j < 3; j++) {
-                const float rz = frcp(s.zq[j]);
-                float gzj = 0.f;
-#pragma unroll
-                for (int qq = 0; qq < 2; qq++) gzj += (-(gpr[qq] * s.dt)) * (w[j] * uvs[2 * j + qq]) * rz * rz;
-                gzj += (-g_st) * w[j] * rz * rz;
-                q.gz[j] = gzj;
+                const float inner = __builtin_fmaf(-gpr[0], uvs[2 * j], __builtin_fmaf(-gpr[1], uvs[2 * j + 1], g_dt * s.dt));
+                q.gz[j] = (w[j] * (rq[j] * rq[j])) * inner;
             }
         }
         if (sh.draw & NR_DRAW_DEPTH) {
@@ -479,13 +472,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             // runtime-indexed register array would go to scratch)
             const int dc = (rgb ? 3 : 0) + ((sh.draw & NR_DRAW_SILHOUETTES) ? 1 : 0);
             const float gd = dc == 4 ? G[4] : dc == 3 ? G[3] : dc == 1 ? G[1] : G[0];
-            const float g_s = -gd * (dep * dep);
-            const float z[3] = {f.z0, f.z1, f.z2};
+            // d dep / d z_k = dep^2 w_k / z_k^2 (the record's 1 / z_k)
+            const float e = gd * (dep * dep);
+            const float rz[3] = {f.rz0, f.rz1, f.rz2};
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const float rz = frcp(z[j]);
-                q.gz[j] += (-g_s) * w[j] * rz * rz;
-            }
+            for (int j = 0; j < 3; j++) q.gz[j] = __builtin_fmaf(w[j] * (rz[j] * rz[j]), e, q.gz[j]);
         }
         // channel values in merge order (rgb, sil, depth), compile-time slots as in shade_pixel
         const bool R = rgb, Sl = (sh.draw & NR_DRAW_SILHOUETTES) != 0;

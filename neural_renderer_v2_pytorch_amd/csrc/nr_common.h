@@ -207,6 +207,10 @@ __device__ __forceinline__ float lane_value(float v, int l) {
 __device__ __forceinline__ bool in_range(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }
 // coordinate / depth magnitudes for which the face-level guard below holds: 0 or [2^-20, 2^20]
 __device__ __forceinline__ bool coord_ok(float x) { return x == 0.f || in_range(x, 0x1p-20f, 0x1p20f); }
+// the face record's reciprocals: rcp_nr inside the exact-division range (the only values the exact
+// paths read, under the face's range flags), the IEEE 1 / x outside it (1 / 0 = inf, as v_rcp; the
+// backward's gradient terms use these for every face)
+__device__ __forceinline__ float face_rcp(float x) { return in_range(x, 0x1p-20f, 0x1p20f) ? rcp_nr(x) : 1.f / x; }
 
 // compute_weight_map_cuda_kernel (.cu:286-306).  Returns true when the weights are known to lie in
 // {0} u [2^-84, 1] (the exact-division path was taken), which the texture and depth stages below
@@ -383,17 +387,17 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
             t0 = tc[off[0]], t1 = tc[off[1]], t2 = tc[off[2]], t3 = tc[off[3]];
         }
         s.rgb[c] = ((s.wt[0] * t0 + s.wt[1] * t1) + s.wt[2] * t2) + s.wt[3] * t3;
-        if (G) {
+        if (G) {  // gradient-only terms: fused multiply-adds (within the gradient tolerance)
             if (c == 0) {
                 gw[0] = G[0] * t0;
                 gw[1] = G[0] * t1;
                 gw[2] = G[0] * t2;
                 gw[3] = G[0] * t3;
             } else {
-                gw[0] = gw[0] + G[c] * t0;
-                gw[1] = gw[1] + G[c] * t1;
-                gw[2] = gw[2] + G[c] * t2;
-                gw[3] = gw[3] + G[c] * t3;
+                gw[0] = __builtin_fmaf(G[c], t0, gw[0]);
+                gw[1] = __builtin_fmaf(G[c], t1, gw[1]);
+                gw[2] = __builtin_fmaf(G[c], t2, gw[2]);
+                gw[3] = __builtin_fmaf(G[c], t3, gw[3]);
             }
         }
     }

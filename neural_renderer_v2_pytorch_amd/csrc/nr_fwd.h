@@ -60,8 +60,8 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                 float4* rec = reinterpret_cast<float4*>(s_frec + t * FACE_REC);
                 rec[0] = make_float4(c[0], c[1], c[2], c[3]);
                 rec[1] = make_float4(c[4], c[5], c[6], c[7]);
-                rec[2] = make_float4(c[8], rcp_nr(c[2]), rcp_nr(c[5]), rcp_nr(c[8]));
-                rec[3] = make_float4(rcp_nr(c[2] + 1e-10f), rcp_nr(c[5] + 1e-10f), rcp_nr(c[8] + 1e-10f),
+                rec[2] = make_float4(c[8], face_rcp(c[2]), face_rcp(c[5]), face_rcp(c[8]));
+                rec[3] = make_float4(face_rcp(c[2] + 1e-10f), face_rcp(c[5] + 1e-10f), face_rcp(c[8] + 1e-10f),
                                      __int_as_float(flags));
                 if (fnorm) {
                     // face normal cross(v1 - v0, v2 - v1) (rasterize.py:166-170; torch.cross component order)

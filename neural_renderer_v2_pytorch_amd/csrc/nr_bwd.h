@@ -401,17 +401,12 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                     q.wy = (int)floorf(s.lo[1]);
                 }
                 const int dx = ix0 - q.wx, dy = iy0 - q.wy;
-                // corners with nonzero weight inside the window and the texture (no row wrap)
-                bool fits = wok;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const float wt = ((i & 2) ? q.by : q.ay) * ((i & 1) ? q.bx : q.ax);
-                    if (wt == 0.f) continue;
-                    const int cx = dx + (i & 1), cy = dy + (i >> 1);
-                    const int gx_ = ix0 + (i & 1), gy_ = iy0 + (i >> 1);
-                    fits = fits && cx >= 0 && cx < TWIN && cy >= 0 && cy < TWIN && gx_ >= 0 && gy_ >= 0 &&
-                           gx_ < sh.tv.W && gy_ < sh.tv.H;
-                }
+                // all four corners inside the window and the texture (no row wrap).  Conservative: a
+                // corner of zero weight outside them also sends the sample to the direct atomics below,
+                // which handle any sample (it can only happen when x or y is a whole number at the
+                // window's or the texture's last column / row)
+                const bool fits = wok && (unsigned)dx <= (unsigned)(TWIN - 2) && (unsigned)dy <= (unsigned)(TWIN - 2) &&
+                                  (unsigned)ix0 < (unsigned)(sh.tv.W - 1) && (unsigned)iy0 < (unsigned)(sh.tv.H - 1);
 #ifdef NR_COUNT_DIRECT
                 atomicAdd(&g_ncount[fits ? 0 : 1], 1ull);
                 if (!fits && !wok) atomicAdd(&g_ncount[2], 1ull);

@@ -363,11 +363,18 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
                 // no operand moves): (c1, c3) = (yp - (y0, y2)) (A, E) - (B, F) (xp - (x0, x2)),
                 // c2 = (yp - y1) C - D (xp - x1); pass unless c1 c2 < 0 or c2 c3 < 0
                 const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
+#if NR_FWD_SCALAR_EDGE
+                const float c1 = (yp - q2.x) * q3.x - q3.z * (xp - q2.z);
+                const float c3 = (yp - q2.y) * q3.y - q3.w * (xp - q2.w);
+                const float c2 = (yp - q4.x) * q4.z - (xp - q4.y) * q4.w;
+                cov = lane_mask_uge(c1 * c2, 0.f) & lane_mask_uge(c3 * c2, 0.f) & pre;
+#else
                 const f32x2 c13 = (f32x2{yp, yp} - f32x2{q2.x, q2.y}) * f32x2{q3.x, q3.y} -
                                   f32x2{q3.z, q3.w} * (f32x2{xp, xp} - f32x2{q2.z, q2.w});
                 const f32x2 t2 = (f32x2{yp, xp} - f32x2{q4.x, q4.y}) * f32x2{q4.z, q4.w};
                 const f32x2 p = c13 * (t2.x - t2.y);
                 cov = lane_mask_uge(p.x, 0.f) & lane_mask_uge(p.y, 0.f) & pre;
+#endif
             }
             if (cov & occ) {  // commit first where this face would queue behind a pending one
                 if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);

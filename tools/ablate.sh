@@ -2,6 +2,8 @@
 # builds one library per variant (comma-separated -D defines; "base" = none) and benches each;
 # CONFIGS=cfg2,cfg3,cfg5 also times those configs (tools/bench_configs.py).
 set -o pipefail
+# the product's hipcc flags (__graft_entry__.HIPCC_FLAGS without -I); HIPFLAGS overrides them
+HIPFLAGS=${HIPFLAGS:-$(cd "$(dirname "$0")/.." && python3 -c 'import __graft_entry__ as g; print(" ".join(g.hipcc_flags()))')}
 cd $GRAFT_REPO_ROOT
 TAG=${1:-ablate}
 OUT=gpurun_out/$TAG
@@ -14,8 +16,8 @@ for V in $VARIANTS; do
   if [ "${V#lib:}" != "$V" ]; then cp "${V#lib:}" $OUT/lib/libnr_$i.so || exit 1; continue; fi
   DEFS=""
   if [ "$V" != base ]; then for d in ${V//,/ }; do DEFS="$DEFS -D$d"; done; fi
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math \
-    -fvisibility=hidden -Iinclude $DEFS neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip -o $OUT/lib/libnr_$i.so || exit 1
+  /opt/rocm/bin/hipcc $HIPFLAGS \
+  -Iinclude $DEFS neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip -o $OUT/lib/libnr_$i.so || exit 1
 done
 # REPEAT=n runs the whole variant list n times, interleaved (box-to-box and run-to-run spread is a
 # few per cent); STEPS sets the timed steps per run

@@ -4,8 +4,9 @@ python tools/count_direct.py"""
 import ctypes, os, subprocess, sys
 ROOT = "/root/repo" if os.path.exists("/root/repo") else os.getcwd()
 lib = "/tmp/libnr_count.so"
-subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-                       "-fno-fast-math", "-fvisibility=hidden", "-DNR_COUNT_DIRECT", "-I" + ROOT + "/include",
+sys.path.insert(0, ROOT)
+import __graft_entry__  # the product's hipcc flags
+subprocess.check_call(["/opt/rocm/bin/hipcc", *__graft_entry__.hipcc_flags(), "-DNR_COUNT_DIRECT", "-I" + ROOT + "/include",
                        ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib])
 os.environ["NR_LIB_PATH"] = lib
 sys.path.insert(0, ROOT); sys.path.insert(0, ROOT + "/tools")

@@ -16,8 +16,9 @@ WORKLOAD = "headline"
 if len(sys.argv) > 2 and sys.argv[1] == "--workload":
     WORKLOAD = sys.argv[2]
     del sys.argv[1:3]
-subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                       "-ffp-contract=off", "-fno-fast-math", "-fvisibility=hidden", "-DNR_FWD_TIMING", "-I" + ROOT + "/include"]
+sys.path.insert(0, ROOT)
+import __graft_entry__  # noqa: E402  (the product's hipcc flags)
+subprocess.check_call(["/opt/rocm/bin/hipcc", *__graft_entry__.hipcc_flags(), "-DNR_FWD_TIMING", "-I" + ROOT + "/include"]
                       + sys.argv[1:] + [ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib_path])
 os.environ["NR_LIB_PATH"] = lib_path
 sys.path.insert(0, ROOT)

@@ -189,10 +189,6 @@ __device__ __forceinline__ float pix_center(int i, int S) {
     if ((S & (S - 1)) == 0) return __builtin_ldexpf((float)(2 * i + 1 - S), -__builtin_ctz((unsigned)S));
     return pix_center_div(i, S);
 }
-// two-wide float vector: elementwise operators compile to packed fp32 instructions (v_pk_add_f32,
-// v_pk_mul_f32), each half rounded exactly as the scalar operation (contraction is off)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
 // lanes (of the active ones) where a >= b or a, b unordered, i.e. !(a < b) / where a <= b or
 // unordered, i.e. !(a > b): the comparison's own lane mask (llvm.amdgcn.fcmp, predicates UGE = 11,
 // ULE = 13), with no per-lane boolean in between

@@ -213,11 +213,10 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 //   tests rows 0-1, issued first), the commit rows 1 and 3-6:
 //     0: xmin xmax ymin ymax | 1: zmin k0 k2 k1 | 2: y0 y2 x0 x2 | 3: A=x1-x0 E=x0-x2 B=y1-y0 F=y0-y2
 //     4: y1 x1 C=x2-x1 D=y2-y1 | 5: z0 z1 z2 id | 6: 1/z0 1/z1 1/z2 ok
-//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit).  Every
-//   pair the edge tests and weights combine sits in an aligned register pair of one row -- (y0, y2),
-//   (x0, x2), (A, E), (B, F), (y1, x1), (C, D), (k2, k1) -- and is evaluated as a two-wide vector
-//   (packed fp32 instructions, each half rounded as the scalar form, no register moves: v38 had 8
-//   moves per walked face).
+//   (y1-y2 = -D etc. exactly, so w0 = (yp*C - xp*D) + k0 reproduces .cu:130 bit for bit).  The edge
+//   tests and weights are scalar f32 instructions: packed ones (v_pk_*_f32, v42-v45) issue in 4
+//   cycles, the rate of two scalar ones, and their operand pairs cost copies of xp and yp (scalar:
+//   headline fwd 0.157 -> 0.152 ms, same-box A/B).
 constexpr int FREC = 7;  // float4 per staged face
 // staged faces per round: 160 for the 256-thread variant (8 blocks per CU need <= 20 KB of LDS;
 // 128 -> 160: headline fwd 0.208 -> 0.195 ms), 512 for the 1024-thread one (2 blocks per CU: up to
@@ -282,12 +281,10 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
     asm volatile("" ::"v"(q1.w), "v"(q5.x), "v"(q5.y), "v"(q5.z), "v"(q5.w), "v"(q6.x), "v"(q6.y), "v"(q6.z), "v"(q6.w));
     if (depth_min < q1.x) return;
     const float z0 = q5.x, z1 = q5.y, z2 = q5.z;
-    // .cu:130-132 as pairs (each half rounded as the scalar form): (w2, w1) = (yp (A, E) - xp (B, F))
-    // + (k2, k1), w0 = (yp C - xp D) + k0
-    const f32x2 w21 = (f32x2{yp, yp} * f32x2{q3.x, q3.y} - f32x2{xp, xp} * f32x2{q3.z, q3.w}) + f32x2{q1.z, q1.w};
-    const f32x2 t0 = f32x2{yp, xp} * f32x2{q4.z, q4.w};
-    float w0 = (t0.x - t0.y) + q1.y;
-    float w1 = w21.y, w2 = w21.x;
+    // .cu:130-132: w2 = (yp A - xp B) + k2, w1 = (yp E - xp F) + k1, w0 = (yp C - xp D) + k0
+    float w2 = (yp * q3.x - xp * q3.z) + q1.z;
+    float w1 = (yp * q3.y - xp * q3.w) + q1.w;
+    float w0 = (yp * q4.z - xp * q4.w) + q1.y;
     const float ws = w0 + w1 + w2;
     float zp;
     if (__float_as_int(q6.w) && in_range(ws, 0x1p-20f, 0x1p20f)) {  // as face_test
@@ -359,22 +356,13 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
                                            lane_mask_ule(xp, q0.y) & lane_mask_uge(yp, q0.z) & lane_mask_ule(yp, q0.w);
             unsigned long long cov = 0;
             if (pre) {
-                // .cu:107-116 as register pairs (rows 1-3 hold each pair's operands side by side, so
-                // no operand moves): (c1, c3) = (yp - (y0, y2)) (A, E) - (B, F) (xp - (x0, x2)),
-                // c2 = (yp - y1) C - D (xp - x1); pass unless c1 c2 < 0 or c2 c3 < 0
+                // .cu:107-116: c1 = (yp - y0) A - B (xp - x0), c3 = (yp - y2) E - F (xp - x2),
+                // c2 = (yp - y1) C - (xp - x1) D; pass unless c1 c2 < 0 or c2 c3 < 0
                 const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
-#if NR_FWD_SCALAR_EDGE
                 const float c1 = (yp - q2.x) * q3.x - q3.z * (xp - q2.z);
                 const float c3 = (yp - q2.y) * q3.y - q3.w * (xp - q2.w);
                 const float c2 = (yp - q4.x) * q4.z - (xp - q4.y) * q4.w;
                 cov = lane_mask_uge(c1 * c2, 0.f) & lane_mask_uge(c3 * c2, 0.f) & pre;
-#else
-                const f32x2 c13 = (f32x2{yp, yp} - f32x2{q2.x, q2.y}) * f32x2{q3.x, q3.y} -
-                                  f32x2{q3.z, q3.w} * (f32x2{xp, xp} - f32x2{q2.z, q2.w});
-                const f32x2 t2 = (f32x2{yp, xp} - f32x2{q4.x, q4.y}) * f32x2{q4.z, q4.w};
-                const f32x2 p = c13 * (t2.x - t2.y);
-                cov = lane_mask_uge(p.x, 0.f) & lane_mask_uge(p.y, 0.f) & pre;
-#endif
             }
             if (cov & occ) {  // commit first where this face would queue behind a pending one
                 if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);

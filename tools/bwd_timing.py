@@ -56,3 +56,13 @@ for k in (1, 2, 3, 4, 6, 8):
             k, sel.sum(), d[:, :, 5][sel].mean(), np.median(d[:, :, 5][sel]), life[sel].mean()))
 starts = np.sort(t[:, :, 0].min(axis=1) - t[:, :, 0].min())
 print("block start times (clocks) p10/p50/p90: %s" % np.percentile(starts, [10, 50, 90]).round())
+# SIMD slots a block holds idle: its four waves share the block's LDS until the last one ends, so a
+# wave that ends early leaves its slot empty for (block end - wave end)
+fg = life.max(axis=1) > 0
+end = t[fg][:, :, 6]
+bend = end.max(axis=1, keepdims=True)
+start = t[fg][:, :, 0]
+held = (bend - start).sum()
+idle = (bend - end).sum()
+print("foreground blocks %d: slot time idle after a wave's end %.3f of the time the block holds its slots"
+      % (fg.sum(), idle / held))

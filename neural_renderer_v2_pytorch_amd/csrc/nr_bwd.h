@@ -659,8 +659,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             uint32_t mine = ((uint32_t)(m0 >> (16 * chunk)) & 0xffffu) | (((uint32_t)(m1 >> (16 * chunk)) & 0xffffu) << 16);
             const float* rbase = rec + 16 * NPX * chunk * REC;
             // one member's contribution: its loads issued together, accumulation predicated (no branch)
-            auto member = [&](int bit, bool on) {
-                const float* r = rbase + bit * REC;
+            auto member = [&](const float* r, bool on) {
                 const float4 ra = reinterpret_cast<const float4*>(r)[0];  // corner weights w00 w01 w10 w11
                 const float4 rb = reinterpret_cast<const float4*>(r)[1];  // G_r G_g G_b pos (G_r, G_g a register pair)
                 const float rf = r[fsel];
@@ -677,7 +676,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                 // of 0x33; d & 31 is 6..31 for every other d in -10..15 and for POS_NONE
                 const int pos = __float_as_int(rb.w);
                 const int d = tt - pos;
-                const bool hit = on && ((0x33u >> (d & 31)) & 1u);
+                const bool hit = on && __builtin_amdgcn_ubfe(0x33u, (unsigned)d, 1u);  // (0x33 >> (d & 31)) & 1
                 const float wsel = (d & 4) ? ((d & 1) ? ra.w : ra.z) : ((d & 1) ? ra.y : ra.x);
                 const float wt = hit ? wsel : 0.f;
                 // fused multiply-adds (gradient sums; 3 of the step's 24 VALU: bwd 0.212 -> 0.207 ms)
@@ -688,7 +687,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                 if (LIT) an += on ? rw * rn : 0.f;  // corner-normal gradient tt = 3 corner + axis
             };
             // one loop over both pixel rows (2- and 4-member steps measured slower)
-            for (; mine; mine &= mine - 1) member(__builtin_ctz(mine), true);
+            for (; mine; mine &= mine - 1) member(rbase + __builtin_ctz(mine) * REC, true);
         }
         // reduce-scatter over the 4 member chunks (lanes t, t+16, t+32, t+48) with the gfx950 lane
         // swaps (VALU, no LDS round trip): lane (t, c) ends with the chunk total of value c

@@ -13,7 +13,8 @@ namespace {
 //      gradient G of the block + halo into LDS (Differentiation saved the images; the flip/AA
 //      backward is an index map and /4), and for the block's own pixels the gradient terms that do
 //      not depend on the stencil (depth and texture-coordinate paths to z, bilinear weights);
-//   2. the soft-gradient stencil (gx, gy) of Differentiation.backward, then the coordinate-map chain
+//   2. the soft-gradient stencil (gx, gy) of Differentiation.backward from per-pair dot products (each
+//      neighbour pair computed once, in LDS, for both its pixels), then the coordinate-map chain
 //      rule -> a 9-float gradient of the gathered face (rasterize.py:232);
 //   3. reduction without LDS float atomics (ds_add_f32 runs at ~3 cycles per lane on gfx950,
 //      tools/ubench_lds_atomics.hip): each lane stages its two pixel records in LDS; the wave groups
@@ -124,23 +125,19 @@ __device__ __forceinline__ float diff_dot(const float* d, const float* g, int C)
         if (c < C) s = s + d[c] * g[c];
     return s;
 }
-// Each neighbour pair's channel differences serve both of its one-sided terms (axis_grad,
-// nr_shade.h): with dp = I0 - Ip, -pair_dot(Ip, I0, G0) = -sum (-dp) G0 = sum dp G0 exactly (negation
-// is exact and round-to-nearest is symmetric), and likewise for the (i - 1, i) pair; only the sign of
-// an all-zero sum can differ, which no caller observes (pick_grad compares, and it is added to gF).
-__device__ __forceinline__ float stencil(const BwdArgs& a, const float* Im, const float* I0, const float* Ip,
-                                         const float* Gm, const float* G0, const float* Gp, int i, int n, int C) {
+// Differentiation.backward's stencil at position i of n along one axis (axis_grad, nr_shade.h), from
+// its two neighbour pairs' channel dot products: p = (dp . G(i + 1), dp . G(i)) of the pair (i, i + 1)
+// and m = the same of the pair (i - 1, i), with dp = I(first) - I(second).  axis_grad's one-sided
+// terms are these exactly: -pair_dot(Ip, I0, G0) = -sum (-dp) G0 = sum dp G0 (negation is exact and
+// round-to-nearest is symmetric), and its (i - 1, i) terms are the left pair's; only the sign of an
+// all-zero sum can differ, which no caller observes (pick_grad compares, and it is added to gF).  Each
+// pair is computed once and serves both of its pixels (k_raster_bwd step 2).
+__device__ __forceinline__ float stencil_pair(const BwdArgs& a, float2 p, float2 m, int i, int n) {
     const bool has_p = i <= n - 2, has_m = i >= 1;
-    float dp[MAXC], dm[MAXC];
-#pragma unroll
-    for (int c = 0; c < MAXC; c++) {
-        dp[c] = I0[c] - Ip[c];
-        dm[c] = Im[c] - I0[c];
-    }
-    const float r_i = has_p ? div_step(a, -diff_dot(dp, Gp, C)) : 0.f;
-    const float r_m = has_m ? div_step(a, -diff_dot(dm, G0, C)) : 0.f;
-    const float l_i = has_p ? div_step(a, diff_dot(dp, G0, C)) : 0.f;
-    const float l_m = has_m ? div_step(a, diff_dot(dm, Gm, C)) : 0.f;
+    const float r_i = has_p ? div_step(a, -p.x) : 0.f;
+    const float r_m = has_m ? div_step(a, -m.x) : 0.f;
+    const float l_i = has_p ? div_step(a, p.y) : 0.f;
+    const float l_m = has_m ? div_step(a, m.y) : 0.f;
     return pick_grad(r_i + r_m, l_m + l_i);
 }
 
@@ -538,6 +535,48 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 
     // ---- 2. Differentiation.backward stencil -> coordinate-map gradient ------------------------
     float gF[NPX][9];
+    // Each neighbour pair's two channel dot products serve both of its pixels (stencil_pair): every
+    // pixel computes the pair with its right and its lower neighbour, the tile's left halo column and
+    // top halo row have theirs computed by lanes of waves 0 and 1, and after a barrier each foreground
+    // pixel combines its four pairs -- half the dot products of a per-pixel stencil, the same values
+    // (bwd 0.207 -> 0.204 ms with the 24-bit index multiplies, same-box A/B, 5 runs each)
+    float2* s_px = reinterpret_cast<float2*>(s_raw + (BWD_LDS_IG + BWD_LDS_HALO) / 4);  // [HN]: pair (i, i + 1)
+    float2* s_py = s_px + HN;                                                            // [HN]: pair (i, i + row)
+    static_assert(BWD_LDS_IG + BWD_LDS_HALO + 2 * HN * 8 <= bwd_lds<LIT>(), "pair terms fit the block's LDS");
+#pragma unroll
+    for (int k = 0; k < NPX; k++) {
+        const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
+        float I0[MAXC], G0[MAXC], dx[MAXC], dy[MAXC], Gx[MAXC], Gy[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; c++) {
+            const bool u = c < C;
+            I0[c] = u ? s_I[c][li] : 0.f; G0[c] = u ? s_G[c][li] : 0.f;
+            dx[c] = u ? I0[c] - s_I[c][li + 1] : 0.f; Gx[c] = u ? s_G[c][li + 1] : 0.f;
+            dy[c] = u ? I0[c] - s_I[c][li + HW_] : 0.f; Gy[c] = u ? s_G[c][li + HW_] : 0.f;
+        }
+        s_px[li] = make_float2(diff_dot(dx, Gx, C), diff_dot(dx, G0, C));
+        s_py[li] = make_float2(diff_dot(dy, Gy, C), diff_dot(dy, G0, C));
+    }
+    {
+        // the pairs whose first pixel is a halo pixel: left column rows 1..BH (wave 0), top row
+        // columns 1..TW (wave 1)
+        const bool lc = t < BH, tr = t >= 64 && t < 64 + TW;
+        if (lc || tr) {
+            const int li = lc ? (t + 1) * HW_ : t - 63, lj = lc ? li + 1 : li + HW_;
+            float d[MAXC], Gi[MAXC], Gj[MAXC];
+#pragma unroll
+            for (int c = 0; c < MAXC; c++) {
+                const bool u = c < C;
+                d[c] = u ? s_I[c][li] - s_I[c][lj] : 0.f;
+                Gi[c] = u ? s_G[c][li] : 0.f;
+                Gj[c] = u ? s_G[c][lj] : 0.f;
+            }
+            const float2 v = make_float2(diff_dot(d, Gj, C), diff_dot(d, Gi, C));
+            if (lc) s_px[li] = v;
+            else s_py[li] = v;
+        }
+    }
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
         BwdPix& q = P[k];
@@ -546,23 +585,8 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         if (q.fi < 0) continue;
         const int py = ty0 + ly0 + 4 * k;
         const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
-        // centre values re-read from LDS (not kept in registers across the barrier)
-        float I0[MAXC], G0[MAXC], Im[MAXC], Ip[MAXC], Gm[MAXC], Gp[MAXC];
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) {
-            const bool u = c < C;
-            I0[c] = u ? s_I[c][li] : 0.f; G0[c] = u ? s_G[c][li] : 0.f;
-            Im[c] = u ? s_I[c][li - 1] : 0.f; Ip[c] = u ? s_I[c][li + 1] : 0.f;
-            Gm[c] = u ? s_G[c][li - 1] : 0.f; Gp[c] = u ? s_G[c][li + 1] : 0.f;
-        }
-        const float gx = stencil(a, Im, I0, Ip, Gm, G0, Gp, px, S, C);
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) {
-            const bool u = c < C;
-            Im[c] = u ? s_I[c][li - HW_] : 0.f; Ip[c] = u ? s_I[c][li + HW_] : 0.f;
-            Gm[c] = u ? s_G[c][li - HW_] : 0.f; Gp[c] = u ? s_G[c][li + HW_] : 0.f;
-        }
-        const float gy = stencil(a, Im, I0, Ip, Gm, G0, Gp, py, S, C);
+        const float gx = stencil_pair(a, s_px[li], s_px[li - 1], px, S);
+        const float gy = stencil_pair(a, s_py[li], s_py[li - HW_], py, S);
         if (wlate && (gx != 0.f || gy != 0.f)) {
             // silhouettes only: the stencil is zero away from silhouette edges, so only these pixels
             // fetch their face and weights (the same computation as in step 1)
@@ -709,7 +733,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             const bool tex_lane = want_tex && chunk < 3 && sw && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
             const bool face_lane = chunk == 3 && tt < 9;
             const float fv = face_lane ? v : pend;
-            float* dst = tex_lane ? gtb + (y * sh.tv.W + x) * 4 + chunk : gFb + key * 9 + tt;
+            float* dst = tex_lane ? gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk : gFb + key * 9 + tt;
             if ((tex_lane || face_lane) && fv != 0.f) unsafeAtomicAdd(dst, fv);
             if (win) {
                 pend = sw ? v : pend + v;
@@ -721,7 +745,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     {  // the last pending window
         const int x = pwx + tdx, y = pwy + tdy;
         if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
-            unsafeAtomicAdd(gtb + (y * sh.tv.W + x) * 4 + chunk, pend);
+            unsafeAtomicAdd(gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk, pend);
     }
     NR_TSTAMP(6);
 #ifdef NR_BWD_TIMING

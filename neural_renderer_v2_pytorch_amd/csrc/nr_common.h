@@ -347,10 +347,13 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
     s.y1 = s.y0 + 1;
     const int xi0 = (int)s.x0, yi0 = (int)s.y0, xi1 = (int)s.x1, yi1 = (int)s.y1;
     const int W = tv.W, HW = tv.H * tv.W;
-    s.idx[0] = yi0 * W + xi0;
-    s.idx[1] = yi0 * W + xi1;
-    s.idx[2] = yi1 * W + xi0;
-    s.idx[3] = yi1 * W + xi1;
+    // 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate): exact for |row| < 2^23 and W < 2^23,
+    // i.e. for any sample inside a texture or one texel past it (the clamp below handles the overhang)
+    const int r0 = __mul24(yi0, W), r1 = __mul24(yi1, W);
+    s.idx[0] = r0 + xi0;
+    s.idx[1] = r0 + xi1;
+    s.idx[2] = r1 + xi0;
+    s.idx[3] = r1 + xi1;
 #pragma unroll
     for (int i = 0; i < 4; i++) s.idx[i] = min(max(s.idx[i], 0), HW - 1);  // weight-0 overhang, SURVEY A9
     s.wt[0] = (s.y1 - s.y) * (s.x1 - s.x);

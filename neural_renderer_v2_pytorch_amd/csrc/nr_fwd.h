@@ -471,7 +471,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         if (ncand == 0) {
             for (int u = wid; u < 16; u += C::NW) {
                 const int px = bx0 + (u & 3) * 8 + (lane & 7), py = by0 + (u >> 2) * 8 + (lane >> 3);
-                if (px < S && py < S) fimb[py * S + px] = -1;
+                if (px < S && py < S) fimb[(int)__umul24(py, S) + px] = -1;
             }
         } else {
             int r = off0;
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                     s_slot[(oy + (lane >> 3)) * COARSE + ox + (lane & 7)] = best >= 0 ? (unsigned short)best : 0xffff;
                 }
                 const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
-                if (px < S && py < S) fimb[py * S + px] = id;
+                if (px < S && py < S) fimb[(int)__umul24(py, S) + px] = id;
             }
         }
     } else {
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
             int ox, oy;
             C::block_of(wid, k, ox, oy);
             const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
-            if (px < S && py < S) fimb[py * S + px] = best[k];
+            if (px < S && py < S) fimb[(int)__umul24(py, S) + px] = best[k];
         }
         if (SHADE && ncand > 0) {
             // the bin's 32x32 face ids go through LDS (the staging area is free once every wave has walked)

@@ -24,12 +24,15 @@ __host__ __device__ __forceinline__ long long halo_item_floats(int S, int C) {
 __host__ __device__ __forceinline__ long long halo_flags_offset_bytes(int B, int S, int C) {
     return (long long)B * halo_item_floats(S, C) * 4;
 }
+// (24-bit multiplies: every factor here is below 2^24 and every offset below 2^31 for the rasters the
+// library accepts; v_mul_lo_u32 would be quarter rate, and every shading wave forms these offsets)
 __device__ __forceinline__ int halo_row_offset(int C, int S, int x, int y, int c) {
-    return (((y / HALO_TH) * 2 + ((y & (HALO_TH - 1)) != 0)) * C + c) * S + x;
+    return (int)__umul24(__umul24((unsigned)((y / HALO_TH) * 2 + ((y & (HALO_TH - 1)) != 0)), C) + c, S) + x;
 }
 __device__ __forceinline__ int halo_col_offset(int C, int S, int x, int y, int c) {
     const int nty = (S + HALO_TH - 1) / HALO_TH, ntx = (S + HALO_TW - 1) / HALO_TW;
-    return nty * 2 * C * S + (((y / HALO_TH) * C + c) * HALO_TH + (y & (HALO_TH - 1))) * (2 * ntx) +
+    return (int)__umul24(__umul24(nty * 2, C), S) +
+           (int)__umul24((__umul24((unsigned)(y / HALO_TH), C) + c) * HALO_TH + (y & (HALO_TH - 1)), 2 * ntx) +
            2 * (x / HALO_TW) + ((x & (HALO_TW - 1)) != 0);
 }
 // offset of channel 0 of tile-border pixel (x, y) and the stride between its channels
@@ -67,7 +70,7 @@ __device__ __forceinline__ void halo_store(float* __restrict__ halo, int b, int 
 __device__ __forceinline__ void shade_quad(const Shade& sh, const float* __restrict__ frb, int b, int S, int iy, int ix,
                                            const int fis[4], float* __restrict__ images, float* __restrict__ halo) {
     const int s = S / 2;
-    const int o = ((S - 2 - iy) >> 1) * s + ((S - 2 - ix) >> 1);
+    const int o = (int)__umul24((S - 2 - iy) >> 1, s) + ((S - 2 - ix) >> 1);
     float* ob = images + (long long)b * sh.C * s * s + o;
     const int ys[4] = {iy + 1, iy, iy + 1, iy}, xs[4] = {ix + 1, ix + 1, ix, ix};
     // the quad's two column and two row centres
@@ -115,7 +118,7 @@ __device__ __forceinline__ void shade_quad(const Shade& sh, const float* __restr
 __device__ __forceinline__ void shade_quad_empty(const Shade& sh, int b, int S, int iy, int ix, float* __restrict__ images,
                                                  float* __restrict__ halo) {
     const int s = S / 2;
-    const int o = ((S - 2 - iy) >> 1) * s + ((S - 2 - ix) >> 1);
+    const int o = (int)__umul24((S - 2 - iy) >> 1, s) + ((S - 2 - ix) >> 1);
     float* ob = images + (long long)b * sh.C * s * s + o;
 #pragma unroll
     for (int c = 0; c < MAXC; c++)

@@ -5,7 +5,8 @@ each barrier-delimited segment.
 
 Weights (MI355X_MICROARCH.md, "Execution model" and the constants table): a wave64 VALU instruction
 issues over 2 cycles on a SIMD-32; packed f32 (v_pk_fma/mul/add_f32) does two lanes' worth per lane
-in 4 (the same f32 rate as two scalar instructions); transcendentals (v_rcp, v_exp, ...) 8.  Moves
+in 4 (the same f32 rate as two scalar instructions); transcendentals (v_rcp, v_exp, ...) and 32-bit
+integer multiplies (v_mul_lo_u32, v_mad_u64_u32, ...) 8.  Moves
 count like any VALU instruction.  The count is static (every branch once, slow paths included), so it
 compares builds of the same source rather than predicting time; since the raster kernels issue-bound
 their foreground waves, a lower count on the hot path has so far always measured faster.
@@ -57,8 +58,8 @@ def metadata(asm, name):
 def weight(op):
     if op.startswith("v_pk_") and "mov" not in op:
         return 4
-    if re.match(r"v_(rcp|rsq|sqrt|exp|log|sin|cos)_", op):
-        return 8
+    if re.match(r"v_(rcp|rsq|sqrt|exp|log|sin|cos)_", op) or re.match(r"v_(mul_lo|mul_hi|mad_u64|mad_i64)_", op):
+        return 8  # transcendental and 32-bit integer multiplies: quarter rate
     return 2
 
 

@@ -7,10 +7,13 @@ atlas (create_textures, 3x288x288, U(0,1)) expanded over the batch; RasterizeHyp
 One step = rasterize_core forward + backward with a fixed N(0,1) upstream gradient (the gradient
 of (images * G).sum()), producing d/dvertices and d/dtextures.
 
-Multi-GPU: one process per GPU (torchrun), each renders its own 64 items (batch sharding, weak
-scaling, no collective on the data path); the timed region is bracketed by barriers and the max
-over ranks is reported.  With N > 1 the rank images are then all-gathered over RCCL (BASELINE cfg4:
-512 items on 8 GPUs "with RCCL gather") and that time is reported separately as gather_ms.
+Multi-GPU: one process per GPU, each renders its own 64 items (batch sharding, weak scaling, no
+collective on the data path); the timed region is bracketed by barriers and the max over ranks is
+reported.  Under torchrun the ranks come from its environment; `bench.py --gpus N` started without
+a launcher spawns the N rank processes itself (before any GPU call) and exits with their status.
+The launched world size must equal --gpus (exit status 2 otherwise).  With N > 1 the rank images
+are then all-gathered over RCCL (BASELINE cfg4: 512 items on 8 GPUs "with RCCL gather") and that
+time is reported separately as gather_ms.
 
 Output: one JSON line on rank 0 (see README/DESIGN for field meanings).
 """
@@ -51,6 +54,57 @@ def parse():
                    help="skip the rocprofv3 --pmc passes that measure the roofline's HBM traffic and VALU share")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled pass (internal)
     return p.parse_args()
+
+
+def under_profiler():
+    """True when this process runs under rocprofv3 (its launcher exports ROCPROF_* settings to the
+    profiled program).  A nested rocprofv3 started from here would inherit the outer profiler's
+    preload and initialise the GPU before its own exec, so the in-run PMC passes are skipped."""
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) and exit with the
+    worst child status.  Runs before this process makes any GPU call: the parent only spawns and
+    waits (a process that has initialised the GPU must not hand over to another program)."""
+    import subprocess
+    n = args.gpus
+    if args.dist_backend == "nccl":
+        ndev = torch.cuda.device_count()  # counts devices without initialising the GPU on this image
+        if ndev < n:
+            sys.stderr.write("bench.py: --gpus %d but %d GPU(s) visible; RCCL needs one GPU per rank "
+                             "(use --dist-backend gloo to rehearse with shared GPUs)\n" % (n, ndev))
+            return 2
+    port = str(free_port())
+    argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(argv, env=env, cwd=ROOT))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        sys.stderr.write("bench.py: rank exit codes %s\n" % codes)
+        return bad[0] if bad[0] > 0 else 1
+    return 0
+
+
+def check_world(args):
+    """The launched world size must be the one asked for with --gpus (a torchrun with another
+    --nproc-per-node, or a stray WORLD_SIZE, would otherwise report a different n_gpus)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but the launched world size is %d\n" % (args.gpus, world))
+        sys.exit(2)
 
 
 def setup_dist(args):
@@ -259,8 +313,14 @@ def cpu_baseline(args, budget_s):
     mpx = done * args.image_size ** 2 / t_total / 1e6
     why = ("all %d CPUs this process may use" % threads if threads == allowed else
            "the OMP_NUM_THREADS=%d allotment of the %d CPUs this process may use" % (threads, allowed))
+    # the brute-force scan is embarrassingly parallel over pixels, so the rate at every CPU of the
+    # machine is at most linear in the thread count; stated, not run (the box allots 16 host
+    # threads per GPU, and running 256 would take the other GPUs' share)
+    at_nproc = None if threads >= ncpu else dict(
+        value_upper_bound=mpx * ncpu / threads, threads=ncpu,
+        how="linear extrapolation of the measured rate (an upper bound), not measured")
     return dict(value=mpx, unit="Mpixels/s", cores=threads, kind="port", cpu_model=model, nproc=ncpu,
-                cpus_allowed=allowed, threads_why=why,
+                cpus_allowed=allowed, threads_why=why, at_nproc=at_nproc,
                 sample="%d of the %d items of the headline batch (1 item = 256^2 output, 512^2 internal, %d faces, "
                        "fwd+bwd), %.1f s; oracle/nr_oracle.c brute force (OpenMP, %d threads) + torch-CPU stages"
                        % (done, args.batch, f.shape[0], t_total, threads))
@@ -329,6 +389,12 @@ def main():
     args = parse()
     if args.pmc_child:
         return pmc_child(args)
+    if args.gpus < 1:
+        sys.stderr.write("bench.py: --gpus must be >= 1\n")
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    check_world(args)
     world, rank, dev = setup_dist(args)
     w = workload(args, rank, dev)
     for _ in range(args.warmup):
@@ -410,7 +476,11 @@ def main():
     # run (rank 0 at N = 1, like the CPU baseline)
     pmc, pmc_note = None, "not measured (N > 1 or --no-pmc)"
     if world == 1 and rank == 0 and not args.no_pmc:
-        pmc, pmc_note = pmc_passes(args)
+        if under_profiler():
+            pmc_note = ("not measured: bench.py runs under rocprofv3 (ROCPROF_* in the environment); a nested "
+                        "profiler pass would inherit the outer one's preload")
+        else:
+            pmc, pmc_note = pmc_passes(args)
     traffic = valu_busy = valu_insts = wait_share = None
     if pmc is not None:
         traffic = pmc.get("hbm_bytes_per_launch", {}).get(dominant)

@@ -56,6 +56,10 @@ NR_API int nr_version(void);
 /* sizeof(NrRasterArgs), for bindings to check their mirror of the struct */
 NR_API size_t nr_raster_args_size(void);
 
+/* ABI version of this header: 4 (nr_last_launch added; 3: workspace_zeroed of nr_rasterize_backward).
+ * Bindings check it, and nr_raster_args_size(), before the first call. */
+#define NR_ABI_VERSION 4
+
 /* Scratch bytes needed by the face-index map for B items, F faces, S x S internal pixels
  * (per-face screen bounding boxes + coarse-bin face bitmasks). */
 NR_API size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size);
@@ -104,7 +108,11 @@ typedef struct NrRasterArgs {
     long long vt_batch_stride;
     int num_vertices_textures;
     const int32_t* faces_textures;  /* [F, 3] */
-    const float* textures;          /* [Bt, 3, H, W] with the strides below; (h, w) row-contiguous */
+    const float* textures;          /* [Bt, 3, H, W] with the strides below; (h, w) row-contiguous.
+                                       Texture coordinates must stay inside the texture (within one
+                                       texel past its edge, whose bilinear weight is 0), as the
+                                       reference's to_map indexing requires (it raises IndexError);
+                                       H and W below 2^23 (24-bit texel index arithmetic). */
     long long tex_stride_b, tex_stride_c, tex_stride_p; /* p = flat texel index h * W + w */
     int tex_height, tex_width;
     /* saved state, written by forward, read by backward */
@@ -180,8 +188,9 @@ NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num
  * (the batch total when the textures are shared).  Needs args->vertex_offsets/vertex_faces.
  * workspace_zeroed: per call, 1 when the caller guarantees the workspace's accumulators are zero
  * (the forward zeroed them through NrRasterArgs.bwd_workspace and no backward has used it since):
- * the backward then skips its own zero fill; 0 = the backward zero-fills (always correct).  A
- * second backward over the same forward state must pass 0. */
+ * the backward then skips its own zero fill; 0 = the backward zero-fills (always correct).  With 1,
+ * args->bwd_workspace must be `workspace` and args->bwd_workspace_bytes must cover the accumulators
+ * (NR_ERR_ARGS otherwise).  A second backward over the same forward state must pass 0. */
 NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
                                  float* grad_textures, void* workspace, size_t workspace_bytes, int workspace_zeroed,
                                  void* stream);
@@ -239,6 +248,14 @@ NR_API int nr_selftest_division(const float* a, const float* b, float* q_fast, f
  * the stream has been synchronised.  Process-wide state, meant for a single measuring thread. */
 NR_API int nr_profile_enable(int on);
 NR_API int nr_profile_read(const char* kernel, float* ms);
+
+/* Launch record (no reference counterpart; the tests use it to assert which kernel variant ran).
+ * For the most recent launch of `kernel` ("k_raster_fwd" or "k_raster_bwd") in this process
+ * (process-wide, like the profiling hook; torch issues a backward from its autograd thread): block_threads = threads per block (k_raster_fwd: 256 = four 16x16 quadrants per
+ * 32x32 bin, 1024 = one wave per 8x8 block; k_raster_bwd: 256 = 2 pixels per lane, 512 = 1 pixel
+ * per lane) and flags = NR_LAUNCH_* bits.  NR_ERR_ARGS when none was recorded. */
+enum { NR_LAUNCH_FUSED_SHADE = 1, NR_LAUNCH_STATIC_CHANNELS = 2, NR_LAUNCH_TWO_PX_PER_LANE = 4 };
+NR_API int nr_last_launch(const char* kernel, int* block_threads, int* flags);
 
 #ifdef __cplusplus
 }

@@ -25,7 +25,12 @@ EXPORTS = [
     "nr_backward_workspace_bytes", "nr_profile_enable", "nr_profile_read",
     "nr_selftest_division", "nr_halo_bytes", "nr_raster_args_size", "nr_rasterize_backward_params",
     "nr_camera_forward", "nr_camera_backward", "nr_camera_workspace_bytes", "nr_texture_packed_bytes",
+    "nr_last_launch",
 ]
+
+ABI_VERSION = 4  # include/nr_raster.h NR_ABI_VERSION
+
+NR_LAUNCH_FUSED_SHADE, NR_LAUNCH_STATIC_CHANNELS, NR_LAUNCH_TWO_PX_PER_LANE = 1, 2, 4
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
 
@@ -104,6 +109,7 @@ def lib():
     L.nr_halo_bytes.restype = c_size_t
     L.nr_halo_bytes.argtypes = [c_int, c_int, c_int, c_int]
     L.nr_selftest_division.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_void_p]
+    L.nr_last_launch.argtypes = [ctypes.c_char_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
     L.nr_profile_enable.argtypes = [c_int]
     L.nr_profile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(c_float)]
     for name in EXPORTS:
@@ -111,8 +117,23 @@ def lib():
                         "nr_halo_bytes", "nr_raster_args_size", "nr_camera_workspace_bytes",
                         "nr_texture_packed_bytes"):
             getattr(L, name).restype = c_int
+    # a library of another ABI revision (an NR_LIB_PATH override, a stale build) would misread the
+    # arguments (e.g. an older nr_rasterize_backward takes its stream where workspace_zeroed is now)
+    if L.nr_version() != ABI_VERSION or L.nr_raster_args_size() != ctypes.sizeof(NrRasterArgs):
+        raise RuntimeError("neural_renderer_v2_pytorch_amd: %s has ABI version %d with a %d-byte NrRasterArgs; this "
+                           "binding needs version %d and %d bytes (rebuild with __graft_entry__.build())"
+                           % (LIB_PATH, L.nr_version(), L.nr_raster_args_size(), ABI_VERSION,
+                              ctypes.sizeof(NrRasterArgs)))
     _lib = L
     return L
+
+
+def last_launch(kernel):
+    """(threads per block, NR_LAUNCH_* flags) of the latest launch of `kernel` ("k_raster_fwd" or
+    "k_raster_bwd") in this process: the variant the library actually ran."""
+    t, f = c_int(), c_int()
+    check(lib().nr_last_launch(kernel.encode(), ctypes.byref(t), ctypes.byref(f)), "nr_last_launch")
+    return t.value, f.value
 
 
 def check(status, what):

@@ -53,6 +53,14 @@ bool g_prof = false;
 hipEvent_t g_prof_ev[P_N][2];
 bool g_prof_rec[P_N];
 
+// launch record (nr_last_launch): block size and NR_LAUNCH_* flags of the latest raster launches in
+// this process (process-wide: torch runs a backward on its autograd device thread), so tests can
+// assert the variant that actually ran
+struct LaunchRec {
+    int threads = 0, flags = 0;
+};
+LaunchRec g_last_fwd, g_last_bwd;
+
 struct ProfScope {  // records the start/end events of one launch when profiling is on
     int k;
     hipStream_t st;

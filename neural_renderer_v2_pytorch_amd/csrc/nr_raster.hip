@@ -67,7 +67,7 @@ __global__ void k_selftest_div(const float* __restrict__ a, const float* __restr
 extern "C" {
 
 const char* nr_last_error(void) { return g_err.c_str(); }
-int nr_version(void) { return 3; }
+int nr_version(void) { return 4; }
 size_t nr_raster_args_size(void) { return sizeof(NrRasterArgs); }
 
 int nr_num_channels(int draw_flags) {
@@ -144,6 +144,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         // over and the bins are shallow; 1024 when it does not, or when the bins are deep (F per bin
         // at the 32x32 bin granularity as the depth proxy)
         const int rs = vertices ? FACE_REC : 9;
+        g_last_fwd = LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
+                               (fuse && ntf == 256 && sh.C == MAXC ? NR_LAUNCH_STATIC_CHANNELS : 0)};
         if (fuse && ntf == 1024)
             hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
@@ -202,7 +204,9 @@ int nr_face_index_map_forward_safe(const float* faces, int32_t* face_index, int 
 
 int nr_compute_weight_map(const float* faces, const int32_t* face_index_map, float* weight_map, int batch_size,
                           int num_faces, int image_size, void* stream) {
-    if (batch_size < 0 || num_faces < 0 || image_size <= 0) return fail(NR_ERR_ARGS, "bad sizes");
+    // the kernels' pixel centres are exact for S <= 16384 (nr_pixel.h), as in the other entry points
+    if (batch_size < 0 || num_faces < 0 || image_size <= 0 || image_size > 16384)
+        return fail(NR_ERR_ARGS, "bad sizes B=%d F=%d S=%d", batch_size, num_faces, image_size);
     const long long n = (long long)batch_size * image_size * image_size;
     if (n == 0) return NR_OK;
     hipLaunchKernelGGL(k_weight_map, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, faces,
@@ -333,6 +337,9 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     const size_t zero_bytes = lit ? (size_t)((char*)gU - (char*)workspace) : need;
     // ... unless the caller states, for this call, that the forward zeroed them (NrRasterArgs.bwd_workspace)
     const bool prezeroed = workspace_zeroed != 0;
+    if (prezeroed && zero_bytes > 0 && (a->bwd_workspace != workspace || a->bwd_workspace_bytes < zero_bytes))
+        return fail(NR_ERR_ARGS, "workspace_zeroed = 1 needs args->bwd_workspace == workspace with at least %zu bytes "
+                                 "(the buffer the forward zeroed)", zero_bytes);
     if (zero_bytes > 0 && !prezeroed && hipMemsetAsync(workspace, 0, zero_bytes, st) != hipSuccess)
         return check_launch("hipMemsetAsync");
     BwdArgs ba;
@@ -547,6 +554,17 @@ __attribute__((visibility("default"))) int nr_debug_bwd_timing(unsigned long lon
     return NR_OK;
 }
 #endif
+
+int nr_last_launch(const char* kernel, int* block_threads, int* flags) {
+    if (!kernel || !block_threads || !flags) return fail(NR_ERR_ARGS, "null argument");
+    const LaunchRec* r = strcmp(kernel, "k_raster_fwd") == 0 ? &g_last_fwd
+                         : strcmp(kernel, "k_raster_bwd") == 0 ? &g_last_bwd : nullptr;
+    if (!r) return fail(NR_ERR_ARGS, "nr_last_launch: unknown kernel name %s", kernel);
+    if (!r->threads) return fail(NR_ERR_ARGS, "nr_last_launch: no %s launch recorded on this thread", kernel);
+    *block_threads = r->threads;
+    *flags = r->flags;
+    return NR_OK;
+}
 
 int nr_profile_enable(int on) {
     if (on && !g_prof) {

@@ -438,6 +438,8 @@ class Rasterize(torch.autograd.Function):
         bg = (backgrounds, gbg) if backgrounds is not None else None
         a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo, ctx.light, bg,
                   tex4=ctx.tex4)
+        if prezeroed:  # the library checks that the workspace it may skip zeroing is the one the forward zeroed
+            a.bwd_workspace, a.bwd_workspace_bytes = ws.data_ptr(), ws.numel()
         with torch.cuda.device(dev):
             # workspace_zeroed = 1 only for the first backward after the forward zeroed it (no fill)
             _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),

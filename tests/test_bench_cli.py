@@ -1,0 +1,52 @@
+"""bench.py's multi-rank launch (BASELINE cfg4 / the 1-2-4-8 GPU metric).
+
+`python3 bench.py --gpus N` started without a launcher spawns the N rank processes itself, before
+any GPU call, and a launched world size that differs from --gpus is an error (exit status 2).  The
+GPU test runs the real command line with two gloo ranks sharing the box's one GPU; the CPU test
+checks the world-size guard, which fires before anything touches a GPU.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(kw)
+    return env
+
+
+def test_world_size_mismatch_exits_nonzero():
+    """A torchrun-style environment with WORLD_SIZE=2 and --gpus 4: exit status 2 and a message,
+    no bench line."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"],
+                       env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"), cwd=ROOT, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 2, (p.returncode, p.stderr[-500:])
+    assert "launched world size is 2" in p.stderr
+    assert "{" not in p.stdout
+
+
+@pytest.mark.gpu
+def test_bench_cli_two_ranks_gloo():
+    """`bench.py --gpus 2 --dist-backend gloo` on the one-GPU box: the script launches its two
+    ranks, each renders its own 64 headline items, and rank 0 prints one line with n_gpus = 2,
+    global_batch = 128 and the all-gather time of the rank images."""
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--steps", "3", "--warmup", "1", "--no-pmc", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=_env(), cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.returncode, p.stderr[-2000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2
+    assert res["config"]["global_batch"] == 128
+    assert res["config"]["parallelism"] == "batch-sharded dp2"
+    assert res["gather_ms"] is not None and res["gather_ms"] > 0
+    assert res["value"] > 0 and res["steps"] == 3

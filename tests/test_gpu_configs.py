@@ -33,7 +33,8 @@ import torch
 import neural_renderer_v2_pytorch_amd as nr
 from neural_renderer_v2_pytorch_amd import rasterize as nrr
 from neural_renderer_v2_pytorch_amd import synthetic
-from test_gpu_parity import close_grads, close_images
+from neural_renderer_v2_pytorch_amd import _lib
+from test_gpu_parity import close_grads, close_images, oracle_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -115,10 +116,11 @@ def test_cfg2_teapot_full_size_vs_oracle(oracle_mod, dev):
 def test_cfg3_car_subdivided_vs_oracle(oracle_mod, dev):
     """BASELINE cfg3: the ShapeNet car once subdivided (14576 faces), B=64, 256^2 AA, textured rgba
     with the car's own atlas shared by the batch (tests_torch/test_rasterize.py:43-81 renders this
-    car).  One batched forward + backward; items 0, 31, 63 against the oracle: face-index map
-    bit-exact, images, vertex gradients.  A second backward of the same graph with the upstream
-    gradient kept on those three items only gives the shared atlas gradient, checked against the
-    oracle's sum over them."""
+    car).  One batched forward + backward; 16 items (every fourth) against the oracle: face-index
+    map bit-exact, images, vertex gradients.  A second backward of the same graph with the upstream
+    gradient kept on those 16 items only gives the shared atlas gradient, checked against the
+    oracle's sum over them (rasterize.py:144-148 scatter).  The deep bins take the 1024-thread
+    forward (asserted from the library's launch record)."""
     v, f, vt, ft, tex = nr.load_obj(CAR, load_textures=True)
     v, f, vt, ft = synthetic.subdivide(v, f, vt, ft)
     assert f.shape[0] == 14576
@@ -133,23 +135,24 @@ def test_cfg3_car_subdivided_vs_oracle(oracle_mod, dev):
     pv = proj.to(dev).requires_grad_(True)
     img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, hp, return_face_index=True)
     assert img.shape == (B, 4, s, s)
+    assert _lib.last_launch("k_raster_fwd") == (1024, _lib.NR_LAUNCH_FUSED_SHADE)
     counts = _bin_candidates(proj[:4], f, 2 * s)
     assert counts.max() > 512, counts.max()  # deep bins: more than one 512-face staging round
     g = torch.randn(img.shape, generator=torch.Generator().manual_seed(43))
     img.backward(g.to(dev), retain_graph=True)
     assert torch.isfinite(pv.grad).all() and torch.isfinite(leaf.grad).all()
-    items = (0, 31, 63)
-    ref, rfim, rgv, rgt = _oracle(oracle_mod, proj, f, items, s, g, tex_cpu, vt, ft, draw_depth=False)
+    items = list(range(0, B, 4))
+    ref, rfim, rgv, rgt = oracle_batch(oracle_mod, proj, f, g, s, tex_cpu, vt, ft, items=items, draw_depth=False)
     for k, i in enumerate(items):
         assert np.array_equal(fim[i].cpu().numpy(), rfim[k]), "item %d fim: %d px" % (
             i, int((fim[i].cpu().numpy() != rfim[k]).sum()))
         close_images(img[i:i + 1], ref[k:k + 1], "cfg3 item %d images" % i)
         close_grads(pv.grad[i:i + 1], rgv[k:k + 1], "cfg3 item %d grad vertices" % i)
     gm = torch.zeros_like(g)
-    gm[list(items)] = g[list(items)]
+    gm[items] = g[items]
     leaf.grad = None
     img.backward(gm.to(dev))
-    close_grads(leaf.grad, rgt, "cfg3 grad textures (items 0, 31, 63)")
+    close_grads(leaf.grad, rgt, "cfg3 grad textures (16 items)")
 
 
 def _torus_renderer():
@@ -229,14 +232,14 @@ def test_fwd256_multi_round_bins_vs_oracle(oracle_mod, dev):
     proj[..., 0] = proj[..., 0] * 0.06 + 0.013
     proj[..., 1] = proj[..., 1] * 0.06 - 0.021
     S = 512
-    nbins = (S // 32) ** 2
-    assert B * nbins >= 8192 and f.shape[0] / nbins < 40  # nr_raster.hip: the 256-thread variant
     counts = _bin_candidates(proj, f, S)
     assert (counts.reshape(B, -1).max(1) > 2 * 160).all(), counts.reshape(B, -1).max(1)
     params, tex, tex_cpu, vt, ft = _textured(f.shape[0], B, dev, 45)
     pv = proj.to(dev).requires_grad_(True)
     img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
                                   return_face_index=True)
+    # the variant that ran: the fused 256-thread forward with compile-time channels
+    assert _lib.last_launch("k_raster_fwd") == (256, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_STATIC_CHANNELS)
     g = torch.randn(img.shape, generator=torch.Generator().manual_seed(46))
     img.backward(g.to(dev))
     items = (0, 13, 31)
@@ -256,14 +259,13 @@ def test_fwd256_wide_bin_masks_vs_oracle(oracle_mod, dev):
     B = 32
     v, f = synthetic.torus(90, 50)
     F = f.shape[0]
-    S = 512
-    nbins = (S // 32) ** 2
-    assert (F + 31) // 32 > 256 and B * nbins >= 8192 and F / nbins < 40
+    assert (F + 31) // 32 > 256
     proj = _scene(v, B)
     params, tex, tex_cpu, vt, ft = _textured(F, B, dev, 47)
     pv = proj.to(dev).requires_grad_(True)
     img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
                                   return_face_index=True)
+    assert _lib.last_launch("k_raster_fwd") == (256, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_STATIC_CHANNELS)
     g = torch.randn(img.shape, generator=torch.Generator().manual_seed(48))
     img.backward(g.to(dev))
     items = (0, 31)

@@ -17,6 +17,7 @@ import torch
 import neural_renderer_v2_pytorch_amd as nr
 from neural_renderer_v2_pytorch_amd import rasterize as nrr
 from neural_renderer_v2_pytorch_amd import synthetic
+from neural_renderer_v2_pytorch_amd import _lib
 
 pytestmark = pytest.mark.gpu
 
@@ -365,32 +366,60 @@ def test_headline_properties(dev):
     assert float((pv2.grad - pv.grad).abs().max()) <= 1e-4 * float(pv.grad.abs().max())
 
 
-def test_headline_sampled_items_vs_oracle(oracle_mod, dev):
-    """Full headline batch (B=64, 256^2 AA, ico 5120, rgb+sil+depth, shared texture atlas) rendered
-    and differentiated in one batched call; items 0, 21 and 63 compared with the CPU oracle run on
-    that item alone: face-index map bit-exact, images and per-item vertex gradients within the
-    stated tolerances (the shared texture gradient sums all 64 items; it is covered by the golden
-    scenes)."""
+def oracle_batch(oracle_mod, proj, f, g, image_size=256, tex=None, vt=None, ft=None, items=None, chunk=8, **kw):
+    """The CPU oracle over `items` of a batch (all by default), `chunk` items per call: (images,
+    fim, grad vertices, grad of the shared texture).  The texture is one leaf expanded over every
+    chunk, so its gradient accumulates over the items as the reference's expand backward sums the
+    batch's index_put_ scatter (rasterize.py:144-148, utils.py:104-114)."""
+    items = list(range(proj.shape[0])) if items is None else list(items)
+    tx = tex.detach().cpu().clone().requires_grad_(True) if tex is not None else None
+    imgs, fims, gvs = [], [], []
+    for c in range(0, len(items), chunk):
+        idx = items[c:c + chunk]
+        pc = proj[idx].detach().cpu().clone().requires_grad_(True)
+        extra = {}
+        if tx is not None:
+            extra = dict(vertices_textures=torch.as_tensor(vt)[None].expand(len(idx), -1, -1), faces_textures=ft,
+                         textures=tx[None].expand(len(idx), -1, -1, -1))
+        ref, internals = oracle_mod.rasterize_core(pc, f, image_size=image_size, return_internals=True, **extra, **kw)
+        ref.backward(g[idx].cpu())
+        imgs.append(ref.detach())
+        fims.append(internals["fim"].numpy())
+        gvs.append(pc.grad)
+    return torch.cat(imgs), np.concatenate(fims), torch.cat(gvs), (tx.grad if tx is not None else None)
+
+
+def test_headline_full_batch_vs_oracle(oracle_mod, dev):
+    """The full headline batch (B=64, 256^2 AA, ico 5120, rgb+sil+depth, shared texture atlas),
+    rendered and differentiated in one batched call, against the CPU oracle on all 64 items:
+    face-index map bit-exact, images and per-item vertex gradients within the stated tolerances,
+    and the shared texture's gradient -- the sum over the 64 items of the reference's index_put_
+    scatter through to_map (rasterize.py:144-148, utils.py:104-114), which is what the headline
+    bench produces -- against the oracle's sum.  Also asserts the kernel variants that ran (the
+    fused 256-thread forward and the 2-pixel-per-lane backward, both with compile-time channels)."""
     B = 64
     proj, f = _ico_batch(4, B, dev)
     vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
     tex_cpu = torch.rand(tex.shape, generator=torch.Generator().manual_seed(3))
-    tex = tex_cpu.to(dev)
+    leaf = tex_cpu.to(dev).requires_grad_(True)
     pv = proj.to(dev).requires_grad_(True)
     params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
-                               faces_textures=torch.as_tensor(ft, device=dev), textures=tex[None].expand(B, -1, -1, -1))
+                               faces_textures=torch.as_tensor(ft, device=dev), textures=leaf[None].expand(B, -1, -1, -1))
     img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
                                   return_face_index=True)
+    assert _lib.last_launch("k_raster_fwd") == (256, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_STATIC_CHANNELS)
     g = torch.randn(img.shape, generator=torch.Generator().manual_seed(11))
     img.backward(g.to(dev))
-    for i in (0, 21, 63):
-        pc = proj[i:i + 1].clone().requires_grad_(True)
-        ref, internals = oracle_mod.rasterize_core(pc, f, image_size=256, vertices_textures=torch.as_tensor(vt)[None],
-                                                   faces_textures=ft, textures=tex_cpu[None], return_internals=True)
-        ref.backward(g[i:i + 1])
-        assert np.array_equal(fim[i].cpu().numpy(), internals["fim"][0].numpy()), "item %d fim" % i
-        close_images(img[i:i + 1], ref, "item %d images" % i)
-        close_grads(pv.grad[i:i + 1], pc.grad, "item %d grad vertices" % i)
+    torch.cuda.synchronize()
+    assert _lib.last_launch("k_raster_bwd") == (256, _lib.NR_LAUNCH_STATIC_CHANNELS | _lib.NR_LAUNCH_TWO_PX_PER_LANE)
+    ref, rfim, rgv, rgt = oracle_batch(oracle_mod, proj, f, g, 256, tex_cpu, vt, ft)
+    got = fim.cpu().numpy()
+    for i in range(B):
+        assert np.array_equal(got[i], rfim[i]), "item %d fim: %d px" % (i, int((got[i] != rfim[i]).sum()))
+        close_images(img[i:i + 1], ref[i:i + 1], "item %d images" % i)
+        close_grads(pv.grad[i:i + 1], rgv[i:i + 1], "item %d grad vertices" % i)
+    assert int((rfim >= 0).sum()) > 0.2 * rfim.size
+    close_grads(leaf.grad, rgt, "shared texture gradient (sum over 64 items)")
 
 
 def test_tiny_depth_faces_vs_oracle(oracle_mod, dev):

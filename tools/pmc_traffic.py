@@ -8,7 +8,8 @@ lane) -- and the per-unit scale is taken from them.  The rasterizer's own loads 
 face-index reads, 36-B face records), for which the guide calls the scale uncalibrated; the
 corrected figure is reported as the traffic estimate with that caveat.
 
-Writes <dir>/pmc_latest.json (copied into profiles/ for bench.py): {"config": [batch, image_size, level, mode], "hbm_bytes_per_launch":
+Writes <dir>/pmc_latest.json (a summary to keep under profiles/ with the round's name; bench.py imports
+summarize() for its in-run passes and reads no file): {"config": [batch, image_size, level, mode], "hbm_bytes_per_launch":
 {kernel: bytes}, "read_bytes": {...}, "write_bytes": {...}, "raw": {...}, "calibration": {...}}.
 """
 import collections

@@ -1,7 +1,8 @@
 # usage: bash tools/pmc_traffic.sh <tag>: HBM traffic per kernel launch from FETCH_SIZE and WRITE_SIZE,
 # each in its own rocprofv3 --pmc pass (they do not fit one pass on gfx950), over a short bench run,
 # plus a pass for the VALU issue share (SQ_INSTS_VALU, GRBM_GUI_ACTIVE) and the memory-wait share;
-# tools/pmc_traffic.py turns them into profiles/pmc_latest.json (read by bench.py's roofline).
+# tools/pmc_traffic.py turns them into <out>/pmc_latest.json (a per-kernel summary to copy into
+# profiles/ under the round's name; bench.py measures its own roofline traffic in-run and reads no file).
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-traffic}

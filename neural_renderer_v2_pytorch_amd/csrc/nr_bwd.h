@@ -31,6 +31,17 @@ constexpr int TWIN = 4;                       // texel window edge per face
 // pos of a pixel without a window texel: tt - POS_NONE is 16..31 for every window texel tt, so the
 // gather's footprint test (0x33 >> (d & 31)) & 1 rejects it with no separate check
 constexpr int POS_NONE = -16;
+// a texture sample outside its face's window (step 1: large atlases, e.g. ShapeNet image textures)
+// keeps its top-left texel's flat index in `pos` as POS_DIRECT - 32 (index + DIRECT_OFF): again 16
+// mod 32, so the gather rejects it too, and after the gather the wave adds it to the texel
+// accumulator four samples per atomic instruction (step 5)
+constexpr int POS_DIRECT = -48;
+constexpr int DIRECT_OFF = 1 << 22;
+constexpr int DIRECT_MAX_HW = 1 << 25;  // texels per texture with a gradient (nr_rasterize_backward checks)
+__device__ __forceinline__ int direct_pos(int base) {
+    return POS_DIRECT - 32 * min(max(base + DIRECT_OFF, 0), DIRECT_MAX_HW + DIRECT_OFF);
+}
+__device__ __forceinline__ int direct_base(int pos) { return ((POS_DIRECT - pos) >> 5) - DIRECT_OFF; }
 
 // staged record: ay by ax bx | G_rgb[3] pos | gF[9] | pad (20 floats); with lights also dL/dnormal[3]
 // and the weights w[3] at 17..22 (24 floats)
@@ -64,12 +75,10 @@ struct BwdArgs {
     const int32_t* __restrict__ fim;
     const float* __restrict__ grad_images;
     float* __restrict__ grad_faces;   // [B, F, 9] face-corner accumulator
-    // texture gradient, two zero-filled accumulators (or null) that k_vertex_grad / k_tex_out add into
-    // the [Bt, 3, H, W] output: RGBA rows [Bt, HWp, 4] for the per-face window flushes (a face's 4x4
-    // window is 4 cache-line rows) and planes [Bt, 3, H, W] for texels outside a face's window (their
-    // three channels on three lines: the RGBA record serialised them on the ShapeNet car's hot texels)
+    // texture gradient: a zero-filled accumulator of RGBA rows [Bt, HWp, 4] (or null) that
+    // k_vertex_grad / k_tex_out transpose into the [Bt, 3, H, W] output; a face's 4x4 window is 4
+    // cache-line rows, a direct sample's 2x2 footprint two 32-B segments
     float* __restrict__ grad_tex;
-    float* __restrict__ grad_tex_planar;
     int HWp;
     const float* __restrict__ halo;   // halo cache written by the forward, or null (re-shade the halo)
     const uint8_t* __restrict__ binfg; // per (item, 32x32 bin) foreground flags after the halo values, or null
@@ -228,7 +237,6 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     const float* __restrict__ fuvb = sh.face_uv + (sh.uv_bstride ? (long long)b * sh.uv_bstride : 0);
     float* __restrict__ gFb = a.grad_faces + (long long)b * a.F * 9;
     float* __restrict__ gtb = a.grad_tex ? a.grad_tex + (long long)bt * 4 * a.HWp : nullptr;
-    float* __restrict__ gtpb = a.grad_tex_planar ? a.grad_tex_planar + (long long)bt * 3 * a.HW : nullptr;
     // wave wid owns the 16x8 block at (16 (wid & 1), 8 (wid >> 1)); lane -> (lx, ly0) and (lx, ly0 + 4)
     // lanes 16 c .. 16 c + 15 (member chunk c of the gather, step 3) hold the pixels of parity class
     // (x & 1, y & 1) = (c & 1, c >> 1) of the wave's region (8 x 2 of them per pixel k, rows 4 apart):
@@ -418,19 +426,9 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                     if (!fits && dup) atomicAdd(&g_ncount[3], 1ull);
                 }
 #endif
-                if (fits) {
-                    q.pos = dx + 4 * dy;  // window texel of the top-left corner (dx, dy in 0..2)
-                } else {
-                    // outside the face window: direct atomics (texel index as sampled)
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-#pragma unroll
-                        for (int ch = 0; ch < 3; ch++) {
-                            const float v = Gt[ch] * s.wt[i];
-                            if (v != 0.f) unsafeAtomicAdd(gtpb + ch * a.HW + s.idx[i], v);
-                        }
-                    }
-                }
+                // window texel of the top-left corner (dx, dy in 0..2); outside the face window: the
+                // top-left texel's flat index as sampled (row-major, unclamped), added in step 5
+                q.pos = fits ? dx + 4 * dy : direct_pos((int)__mul24(iy0, sh.tv.W) + ix0);
             }
             // texture coordinates -> z.  Gradient-only terms (within the gradient tolerance, they feed
             // no comparison): fused multiply-adds, factored sums, and the face record's reciprocals
@@ -747,6 +745,50 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
             unsafeAtomicAdd(gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk, pend);
     }
+    // ---- 5. texture samples outside their face's window (POS_DIRECT): their texel gradients, 4
+    // samples per atomic instruction.  Lane (sample u = lane >> 4, row = bit 3, column = bit 2,
+    // channel = bits 0-1) adds G_ch * w(row, column) to texel (x0 + column, y0 + row) of RGBA row
+    // storage, so one instruction covers two 32-B segments (the two texel pairs) per sample, where
+    // one texel channel per lane and instruction put every lane in its own 64-B line (the memory-side
+    // atomic units take a line per request: MI355X_MICROARCH.md "Global float atomics").  The
+    // staged records still hold each sample's corner weights, G and position, so no state crosses
+    // the gather loop; the wave's own record region is all it reads.
+    if (want_tex) {
+        unsigned long long d0 = 0ull, d1 = 0ull;
+#pragma unroll
+        for (int k = 0; k < NPX; k++) {
+            const int pos = __float_as_int(rec[(16 * NPX * (lane >> 4) + 16 * k + (lane & 15)) * REC + 7]);
+            const unsigned long long m = __ballot(pos <= POS_DIRECT);
+            if (k == 0) d0 = m;
+            else d1 = m;
+        }
+        const int row = (lane >> 3) & 1, col = (lane >> 2) & 1, ch = lane & 3;
+        const int HW = sh.tv.H * sh.tv.W;
+        while (d0 | d1) {
+            // four samples (wave-uniform slots; -1 when the list runs out), picked on the scalar unit
+            int sl[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool from0 = d0 != 0ull;
+                const unsigned long long m = from0 ? d0 : d1;
+                const int j = m ? __builtin_ctzll(m) : 0;
+                sl[u] = m ? 16 * NPX * (j >> 4) + 16 * (from0 ? 0 : 1) + (j & 15) : -1;
+                if (from0) d0 &= d0 - 1;
+                else d1 &= d1 - 1;
+            }
+            const int u = lane >> 4;
+            const int slot = u == 0 ? sl[0] : u == 1 ? sl[1] : u == 2 ? sl[2] : sl[3];
+            const float* r = rec + max(slot, 0) * REC;
+            const float4 ra = reinterpret_cast<const float4*>(r)[0];  // corner weights w00 w01 w10 w11
+            const float4 rb = reinterpret_cast<const float4*>(r)[1];  // G_r G_g G_b pos
+            const float wsel = row ? (col ? ra.w : ra.z) : (col ? ra.y : ra.x);
+            const float gsel = ch == 0 ? rb.x : (ch == 1 ? rb.y : rb.z);
+            const float v = gsel * wsel;
+            // the texel index as sample_texture clamps it (a clamped corner has weight 0)
+            const int idx = min(max(direct_base(__float_as_int(rb.w)) + col + row * sh.tv.W, 0), HW - 1);
+            if (slot >= 0 && ch < 3 && v != 0.f) unsafeAtomicAdd(gtb + idx * 4 + ch, v);
+        }
+    }
     NR_TSTAMP(6);
 #ifdef NR_BWD_TIMING
     {
@@ -781,7 +823,7 @@ constexpr int VGRAD_UNROLL = 4;
 __global__ void k_vertex_grad(const float* __restrict__ gF, const int32_t* __restrict__ off,
                               const int32_t* __restrict__ ent, float* __restrict__ gV, int F, int V, long long n,
                               TexOut to) {
-    if (to.out) {  // this block's slice of the texture-gradient output (RGBA window sums + planar rest)
+    if (to.out) {  // this block's slice of the texture-gradient output (the RGBA accumulator transposed)
         long long lo, hi;
         grid_slice(to.n, lo, hi);
         for (long long j = lo + threadIdx.x; j < hi; j += blockDim.x) tex_out_one(to, j);

@@ -687,12 +687,11 @@ __device__ __forceinline__ void tex_pack_one(const TexPack& pk, long long i) {
     }
     pk.out[i] = v;
 }
-// The backward's two texture-gradient accumulators (RGBA rows [Bt, HWp, 4] of the per-face window
-// flushes, planes [Bt, 3, H, W] of the other texels) summed into the [Bt, 3, H, W] gradient, carried by
-// k_vertex_grad's blocks (or k_tex_out)
+// The backward's texture-gradient accumulator (RGBA rows [Bt, HWp, 4]: the per-face window flushes and
+// the direct samples) transposed into the [Bt, 3, H, W] gradient, carried by k_vertex_grad's blocks
+// (or k_tex_out)
 struct TexOut {
     const float* __restrict__ g4;
-    const float* __restrict__ planar;
     float* __restrict__ out;   // null: nothing to write
     int HW, HWp;
     long long n;  // Bt * HW
@@ -701,10 +700,9 @@ __device__ __forceinline__ void tex_out_one(const TexOut& to, long long i) {
     const long long bt = i / to.HW;
     const int p = (int)(i % to.HW);
     const float4 v = reinterpret_cast<const float4*>(to.g4)[bt * to.HWp + p];
-    const float* pl = to.planar + bt * 3 * to.HW + p;
-    to.out[(bt * 3 + 0) * to.HW + p] = v.x + pl[0];
-    to.out[(bt * 3 + 1) * to.HW + p] = v.y + pl[to.HW];
-    to.out[(bt * 3 + 2) * to.HW + p] = v.z + pl[2 * to.HW];
+    to.out[(bt * 3 + 0) * to.HW + p] = v.x;
+    to.out[(bt * 3 + 1) * to.HW + p] = v.y;
+    to.out[(bt * 3 + 2) * to.HW + p] = v.z;
 }
 // this block's slice [lo, hi) of n items spread over the whole grid
 // the backward's accumulators, zeroed by the forward's face setup (NrRasterArgs.bwd_workspace)

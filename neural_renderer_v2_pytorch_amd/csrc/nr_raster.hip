@@ -282,14 +282,14 @@ size_t nr_halo_bytes(int batch_size, int image_size, int anti_aliasing, int draw
            (((size_t)batch_size * g.nbins + 3) & ~size_t(3));
 }
 
-// backward workspace: [gF: B F 9 face-corner floats][g4: Bt HWp RGBA texel rows][planar: Bt 3 H W]
+// backward workspace: [gF: B F 9 face-corner floats][g4: Bt HWp RGBA texel rows]
 // [lights: gN: B F 9][gU: B V 3]; everything before gU starts at zero (one memset, or the forward's
 // setup zeroed it: NrRasterArgs.bwd_workspace)
 size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num_vertices, int texture_items,
                                    int tex_height, int tex_width, int num_lights) {
     const size_t hw = (size_t)tex_height * tex_width, hwp = (hw + 3) & ~size_t(3);
     size_t n = align_up((size_t)batch_size * num_faces * 9 * 4);
-    if (texture_items > 0) n += align_up((size_t)texture_items * hwp * 16) + align_up((size_t)texture_items * 3 * hw * 4);
+    if (texture_items > 0) n += align_up((size_t)texture_items * hwp * 16);
     if (num_lights > 0)
         n += align_up((size_t)batch_size * num_faces * 9 * 4) + align_up((size_t)batch_size * num_vertices * 3 * 4);
     return n;
@@ -315,6 +315,10 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     const bool rgb = (a->draw_flags & NR_DRAW_RGB) && grad_textures;
     const bool lit = (a->draw_flags & NR_DRAW_RGB) && a->num_lights > 0;
     const int tex_items = rgb ? (a->tex_stride_b ? a->batch_size : 1) : 0;
+    // texel indices of the backward's direct samples ride in a 32-bit field (nr_bwd.h POS_DIRECT)
+    if (rgb && (long long)a->tex_height * a->tex_width > DIRECT_MAX_HW)
+        return fail(NR_ERR_ARGS, "texture gradient: at most %d texels per texture (got %d x %d)", DIRECT_MAX_HW,
+                    a->tex_height, a->tex_width);
     const size_t need = nr_backward_workspace_bytes(a->batch_size, a->num_faces, a->num_vertices, tex_items,
                                                     a->tex_height, a->tex_width, lit ? a->num_lights : 0);
     if (need > 0 && (!workspace || workspace_bytes < need))
@@ -329,8 +333,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     float* gF = (float*)w;
     w += align_up((size_t)a->batch_size * a->num_faces * 9 * 4);
     float* g4 = rgb ? (float*)w : nullptr;
-    float* gpl = rgb ? (float*)(w + align_up((size_t)tex_items * HWp * 16)) : nullptr;
-    if (rgb) w += align_up((size_t)tex_items * HWp * 16) + align_up((size_t)tex_items * 3 * HW * 4);
+    if (rgb) w += align_up((size_t)tex_items * HWp * 16);
     float* gN = lit ? (float*)w : nullptr;
     float* gU = lit ? (float*)(w + align_up((size_t)a->batch_size * a->num_faces * 9 * 4)) : nullptr;
     // gU is fully written by k_vnormal_bwd; the accumulators before it start at zero
@@ -348,7 +351,6 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.grad_images = grad_images;
     ba.grad_faces = gF;
     ba.grad_tex = g4;
-    ba.grad_tex_planar = gpl;
     ba.halo = a->halo;
     ba.binfg = a->halo ? (const uint8_t*)a->halo + halo_flags_offset_bytes(a->batch_size, S, nr_num_channels(a->draw_flags))
                        : nullptr;
@@ -393,7 +395,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
         }
     }
     TexOut to{};
-    if (rgb) to = TexOut{g4, gpl, grad_textures, HW, HWp, (long long)tex_items * HW};
+    if (rgb) to = TexOut{g4, grad_textures, HW, HWp, (long long)tex_items * HW};
     // k_vertex_grad's blocks also carry the texture-gradient output when that is a few texels per
     // thread; otherwise (no vertices, or a large texture) it gets a launch of its own
     constexpr int VB = 256;  // small blocks: more of them in flight for this latency-bound gather

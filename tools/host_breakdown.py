@@ -1,0 +1,101 @@
+"""Where the host's time per eager step goes (GPU box): the cfg2 teapot step (B=4, the config the
+host's launch path bounds) and the headline step, each timed as a whole and in parts, with the GPU
+kept out of the measurement by timing host enqueue over many steps (the GPU work of cfg2 is ~0.1 ms
+per step, so the queue never fills).
+
+usage: python tools/host_breakdown.py [steps]
+"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import bench_configs  # noqa: E402
+import neural_renderer_v2_pytorch_amd as nr  # noqa: E402
+from neural_renderer_v2_pytorch_amd import _lib  # noqa: E402
+from neural_renderer_v2_pytorch_amd import rasterize as nrr  # noqa: E402
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+
+
+def per_call_us(fn, n=N):
+    for _ in range(20):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    t = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    tall = time.perf_counter() - t0
+    return 1e6 * t / n, 1e6 * tall / n
+
+
+def teapot():
+    v, f = nr.load_obj(os.path.join(bench_configs.DATA, "teapot.obj"))
+    B, s = 4, 256
+    proj = bench_configs.scene(v, f, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex = torch.as_tensor(np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32), device=dev)
+    tex.requires_grad_(True)
+    vt_d, ft_d = torch.as_tensor(vt, device=dev), torch.as_tensor(ft, device=dev)
+    faces = torch.as_tensor(f, device=dev)
+    g = torch.randn((B, 5, s, s), device=dev)
+    return proj, tex, vt_d, ft_d, faces, g, B, s
+
+
+def main():
+    proj, tex, vt_d, ft_d, faces, g, B, s = teapot()
+    out = {}
+
+    def params():
+        return nr.RasterizeParam(vertices_textures=vt_d[None].expand(B, -1, -1), faces_textures=ft_d,
+                                 textures=tex[None].expand(B, -1, -1, -1))
+
+    def step():
+        proj.grad = tex.grad = None
+        nr.rasterize_core(proj, faces, params(), nr.RasterizeHyperparam(image_size=s)).backward(g)
+
+    def fwd_grad():
+        nr.rasterize_core(proj, faces, params(), nr.RasterizeHyperparam(image_size=s))
+
+    def fwd_nograd():
+        with torch.no_grad():
+            nr.rasterize_core(proj, faces, params(), nr.RasterizeHyperparam(image_size=s))
+
+    x = torch.zeros(16, device=dev, requires_grad=True)
+
+    def tiny_autograd():  # the engine's own cost: a one-op graph and its backward
+        (x * 2).sum().backward()
+
+    L = _lib.lib()
+
+    def ctypes_call():
+        L.nr_num_channels(7)
+
+    def empties():
+        for _ in range(8):
+            torch.empty(1024, device=dev)
+
+    def params_only():
+        params()
+        nr.RasterizeHyperparam(image_size=s)
+
+    for name, fn in [("step", step), ("forward (grad on)", fwd_grad), ("forward (no_grad)", fwd_nograd),
+                     ("tiny autograd fwd+bwd", tiny_autograd), ("ctypes call", ctypes_call),
+                     ("8 x torch.empty", empties), ("RasterizeParam + Hyperparam", params_only)]:
+        h, a = per_call_us(fn)
+        out[name] = (h, a)
+        print("%-32s host %8.1f us/call   with GPU %8.1f us/call" % (name, h, a), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -30,7 +30,7 @@ EXPORTS = [
 
 ABI_VERSION = 4  # include/nr_raster.h NR_ABI_VERSION
 
-NR_LAUNCH_FUSED_SHADE, NR_LAUNCH_STATIC_CHANNELS, NR_LAUNCH_TWO_PX_PER_LANE = 1, 2, 4
+NR_LAUNCH_FUSED_SHADE, NR_LAUNCH_STATIC_CHANNELS, NR_LAUNCH_TWO_PX_PER_LANE, NR_LAUNCH_DEEP_FIRST = 1, 2, 4, 8
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
 
@@ -142,7 +142,27 @@ def check(status, what):
 
 
 def stream_of(t):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    """The raw hipStream_t of the current stream on t's device (what torch launches on)."""
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(t.device.index))
+
+
+class on_device:
+    """`with torch.cuda.device(dev)` that costs nothing when dev is already the current device
+    (the usual case: the per-call exchange of the current device was a few microseconds of host
+    time per launch call)."""
+    __slots__ = ("idx", "prev")
+
+    def __init__(self, dev):
+        self.idx = dev.index
+
+    def __enter__(self):
+        cur = torch._C._cuda_getDevice()
+        self.prev = None if cur == self.idx else torch.cuda._exchange_device(self.idx)
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            torch.cuda._exchange_device(self.prev)
+        return False
 
 
 def ptr(t):

@@ -95,9 +95,11 @@ Geom make_geom(int F, int S) {
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-// workspace layout: [bbox int2 B*F][mask u32 B*nbins*nwords]
+// workspace layout: [bbox int2 B*F][mask u32 B*nbins*nwords][bin candidate counts i32 B*nbins]
+// [bin order i32 B*nbins] (the last two: deep-bin dispatch order, run_face_index)
 size_t ws_bbox_bytes(int B, int F) { return align_up((size_t)B * F * sizeof(int2)); }
 size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins * g.nwords * 4); }
+size_t ws_order_bytes(int B, const Geom& g) { return 2 * align_up((size_t)B * g.nbins * 4); }
 
 // ------------------------------------------------------------------------------------------------
 // device helpers
@@ -626,6 +628,18 @@ __device__ __forceinline__ void block_item_tile(int G, int nx, int ny, int& b, i
     }
     b = blockIdx.y;
     xcd_tile(blockIdx.x, b, nx, ny, tx, ty);
+}
+// The (item, bin) of a forward block from the deep-first dispatch order (k_bin_order): with B a
+// multiple of 8, list x (items = x mod 8) is read by the blocks dealt to XCD x (L % 8 = x), so an
+// item's bins stay on one XCD as with block_item_tile; otherwise one list for the whole grid.
+__device__ __forceinline__ void ordered_bin(const int* __restrict__ order, int B, int nbins, int nbx, int& b,
+                                            int& tx, int& ty) {
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int e = (B % 8 == 0) ? order[(L & 7) * ((B >> 3) * nbins) + (L >> 3)] : order[L];
+    b = e / nbins;
+    const int bin = e - b * nbins;
+    ty = bin / nbx;
+    tx = bin - ty * nbx;
 }
 // the interleave group for B items and a preferred group size: the preference when it divides B, else
 // all B items; 0 (per-item bands) when B is not a multiple of 8

@@ -18,7 +18,8 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     uint32_t* __restrict__ mask, int nbx, int nbins, int nwords,
                                                     const float* __restrict__ vt, long long vt_bstride, int Vt,
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
-                                                    int uv_items, float* __restrict__ fnorm, TexPack pk, ZeroFill zf) {
+                                                    int uv_items, float* __restrict__ fnorm, TexPack pk, ZeroFill zf,
+                                                    int* __restrict__ bin_count) {
     __shared__ int2 s_bb[SETUP_FACES];
     // the block's face records, assembled per face and then written out coalesced (a record per lane
     // would store 64-B strided rows); the bin-mask words reuse the space afterwards
@@ -145,6 +146,14 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
             const int bin = p / nw, wi = p % nw;
             mask[((long long)b * nbins + bin) * nwords + w0 + wi] = s_mask[bin * (SETUP_FACES / 32) + wi];
         }
+        if (bin_count) {  // candidate faces per bin (zeroed before the launch), for the deep-first order
+            for (int bin = t; bin < nbins; bin += blockDim.x) {
+                int pc = 0;
+#pragma unroll
+                for (int wi = 0; wi < SETUP_FACES / 32; wi++) pc += __builtin_popcount(s_mask[bin * (SETUP_FACES / 32) + wi]);
+                if (pc) atomicAdd(&bin_count[(long long)b * nbins + bin], pc);
+            }
+        }
         zero_fill(zf);
         return;
     }
@@ -184,6 +193,45 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
     const float len = sqrtf((u0 * u0 + u1 * u1) + u2 * u2);
     const float d = fmaxf(len, 1e-12f);
     reinterpret_cast<float4*>(vnorm)[i] = make_float4(u0 / d, u1 / d, u2 / d, len);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Deep-first dispatch order of the forward's bins (deep-bin launches: the car, the 50k torus).  A bin
+// with thousands of candidate faces keeps its block for 100-500 us while a shallow bin's lasts a few;
+// dispatched in screen order, the deepest bins of the car started up to 360 us into a 790 us kernel and
+// the kernel ended on them (profiles/r04_*_fwd_wave_phases_car.txt).  This orders the (item, bin)
+// pairs by candidate count, descending, in log2 buckets (a stable counting sort: screen order within a
+// bucket), longest first: one list per XCD when B is a multiple of 8 (list x: items = x mod 8, read by
+// the blocks dealt to XCD x, ordered_bin), else one list.  Any order gives the same results: every
+// bin's block is independent.
+__device__ __forceinline__ int count_bucket(int c) { return c <= 0 ? 0 : min(15, 32 - __clz(c)); }
+__global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt, int* __restrict__ order, int B,
+                                                    int nbins) {
+    __shared__ int s_scan[16];
+    const bool per_xcd = gridDim.x == 8;
+    const int x = blockIdx.x;
+    const int items = per_xcd ? B / 8 : B;
+    const int n = items * nbins;
+    const int c = (n + blockDim.x - 1) / blockDim.x;
+    const int lo = threadIdx.x * c, hi = min(lo + c, n);
+    int* __restrict__ out = order + (per_xcd ? x * n : 0);
+    auto entry = [&](int k) {
+        const int j = k / nbins;
+        return (per_xcd ? x + 8 * j : j) * nbins + (k - j * nbins);
+    };
+    int base = 0;
+    for (int bk = 15; bk >= 0; bk--) {
+        int m = 0;
+        for (int k = lo; k < hi; k++) m += count_bucket(cnt[entry(k)]) == bk;
+        int tot;
+        int p = base + block_scan<16>(m, tot, s_scan);
+        if (m)
+            for (int k = lo; k < hi; k++) {
+                const int e = entry(k);
+                if (count_bucket(cnt[e]) == bk) out[p++] = e;
+            }
+        base += tot;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -398,11 +446,12 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
 
 // per-wave phase timestamps of the fused forward (timing builds only, tools/fwd_timing.py)
 #ifdef NR_FWD_TIMING
-constexpr long long NR_FTIMING_MAX = 1 << 21;
+constexpr long long NR_FTIMING_MAX = 1 << 22;
+constexpr int NR_FTSLOTS = 10;  // per wave: 8 phase slots, then the wall clock (100 MHz, chip-wide) at start and end
 __device__ unsigned long long g_fwd_t[NR_FTIMING_MAX];
 #define NR_FTSTAMP(k, v)                                                                                   \
     do {                                                                                                   \
-        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 8 + (k); \
+        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * NR_FTSLOTS + (k); \
         const unsigned long long t_ = (v);                                                                 \
         if ((threadIdx.x & 63) == 0 && i_ < NR_FTIMING_MAX) g_fwd_t[i_] = t_;                       \
     } while (0)
@@ -424,7 +473,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
                                                   int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
-                                                  float* __restrict__ halo, uint8_t* __restrict__ binfg) {
+                                                  float* __restrict__ halo, uint8_t* __restrict__ binfg,
+                                                  const int* __restrict__ order) {
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
@@ -437,7 +487,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 
     const int S = g.S;
     int b, bin_x, bin_y;
-    block_item_tile(g.group, g.nbx, g.nby, b, bin_x, bin_y);
+    if (order) ordered_bin(order, gridDim.y, g.nbins, g.nbx, b, bin_x, bin_y);
+    else block_item_tile(g.group, g.nbx, g.nby, b, bin_x, bin_y);
     const int bin = bin_y * g.nbx + bin_x;
     const int bx0 = bin_x * COARSE;
     const int by0 = bin_y * COARSE;
@@ -449,6 +500,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     int32_t* __restrict__ fimb = fim + (long long)b * S * S;
 
     NR_FTSTAMP(0, clock64());
+    NR_FTSTAMP(8, wall_clock64());
 #ifdef NR_FWD_TIMING
     unsigned long long t_stage = 0;
 #endif
@@ -599,6 +651,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     if (!SHADE) {
         NR_FTSTAMP(4, clock64());
         NR_FTSTAMP(5, clock64());
+        NR_FTSTAMP(9, wall_clock64());
         NR_FTSTAMP(6, (unsigned long long)ncand);
     }
     if (SHADE && ncand == 0) {
@@ -615,6 +668,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         if ((NTF == 256 || t < 256) && iy + 1 < S && ix + 1 < S) shade_quad_empty(sh, b, S, iy, ix, images, binfg ? nullptr : halo);
         NR_FTSTAMP(4, clock64());
         NR_FTSTAMP(5, clock64());
+        NR_FTSTAMP(9, wall_clock64());
         NR_FTSTAMP(6, 0ull);
         return;
     }
@@ -652,6 +706,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
             shade_quad(sh, face_records + (long long)b * F * FACE_REC, b, S, iy, ix, fis, images, halo);
         }
         NR_FTSTAMP(5, clock64());
+        NR_FTSTAMP(9, wall_clock64());
         NR_FTSTAMP(6, (unsigned long long)ncand);
     }
 }

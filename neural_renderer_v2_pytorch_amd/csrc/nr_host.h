@@ -30,7 +30,7 @@ int validate_raster(const NrRasterArgs* a, bool need_workspace) {
         if (span >= (1ll << 31)) return fail(NR_ERR_ARGS, "texture item spans 2^31 elements or more");
     }
     const Geom g = make_geom(a->num_faces, S);
-    const size_t need = ws_bbox_bytes(a->batch_size, a->num_faces) + ws_mask_bytes(a->batch_size, g);
+    const size_t need = ws_bbox_bytes(a->batch_size, a->num_faces) + ws_mask_bytes(a->batch_size, g) + ws_order_bytes(a->batch_size, g);
     if (need_workspace && need > 0 && (!a->workspace || a->workspace_bytes < need))
         return fail(NR_ERR_WORKSPACE, "workspace missing or too small");
     return NR_OK;

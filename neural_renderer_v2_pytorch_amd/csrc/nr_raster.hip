@@ -77,7 +77,7 @@ int nr_num_channels(int draw_flags) {
 
 size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
     const Geom g = make_geom(num_faces, image_size);
-    return ws_bbox_bytes(batch_size, num_faces) + ws_mask_bytes(batch_size, g);
+    return ws_bbox_bytes(batch_size, num_faces) + ws_mask_bytes(batch_size, g) + ws_order_bytes(batch_size, g);
 }
 
 static int run_face_index(const float* vertices, const int32_t* faces_idx, float* face_records, int32_t* fim,
@@ -88,7 +88,21 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     g.group = group_for(B, FWD_GROUP);
     int2* bbox = (int2*)ws;
     uint32_t* mask = (uint32_t*)((char*)ws + ws_bbox_bytes(B, F));
+    int* bin_count = (int*)((char*)mask + ws_mask_bytes(B, g));
+    int* bin_order = (int*)((char*)bin_count + ws_order_bytes(B, g) / 2);
     if (B == 0) return NR_OK;
+    // forward block size (k_raster_fwd notes): 256 threads when the grid alone fills the chip many
+    // times over and the bins are shallow; 1024 when it does not, or when the bins are deep (F per bin
+    // at the 32x32 bin granularity as the depth proxy)
+    const long long blocks = (long long)g.nbins * B;
+    const double faces_per_bin = (double)F / g.nbins;
+    const int ntf = (blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024;
+    // deep bins (the car, the 50k torus): dispatch the bins deepest first (k_bin_order), from candidate
+    // counts the setup adds up (its LDS bin-mask path); a list per XCD needs B % 8 == 0 or fits one block
+    const bool ordered = F > 0 && ntf == 1024 && faces_per_bin >= 24.0 &&
+                         (long long)g.nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS;
+    if (ordered && hipMemsetAsync(bin_count, 0, (size_t)B * g.nbins * 4, st) != hipSuccess)
+        return check_launch("hipMemsetAsync");
     // the setup's idle threads repack the textures when that takes them up to 32 texels each; with no
     // setup launch, or a texture too large for that, the repacking gets a launch of its own
     const long long setup_idle = (long long)((F + SETUP_FACES - 1) / SETUP_FACES) * B * (256 - SETUP_FACES);
@@ -113,11 +127,12 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
-                               rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk, zf);
+                               rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk, zf,
+                               ordered ? bin_count : nullptr);
         else
             hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
-                               nullptr, pk, zf);
+                               nullptr, pk, zf, ordered ? bin_count : nullptr);
         int e = check_launch("k_face_setup");
         if (e) return e;
         if (lit && V > 0) {
@@ -128,11 +143,14 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             if (e) return e;
         }
     }
+    if (ordered) {
+        hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_count, bin_order, B, g.nbins);
+        const int e = check_launch("k_bin_order");
+        if (e) return e;
+    }
+    const int* order = ordered ? bin_order : nullptr;
     // k_shade's work fused into the forward's 256-thread variant (anti-aliasing, no lights or
     // backgrounds): the face-index map is not read back, and there is one launch fewer
-    const long long blocks = (long long)g.nbins * B;
-    const double faces_per_bin = (double)F / g.nbins;
-    const int ntf = (blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024;
     const Shade sh = ra ? make_shade(ra) : Shade{};
     // the deep-bin / small-grid 1024-thread variant shades too (its threads 0-255)
     const bool fuse = ra && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
@@ -140,27 +158,25 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     uint8_t* binfg = (ra && ra->halo) ? (uint8_t*)ra->halo + halo_flags_offset_bytes(B, S, sh.C) : nullptr;
     {
         ProfScope _p(P_RASTER, st);
-        // block size (k_raster_fwd notes): 256 threads when the grid alone fills the chip many times
-        // over and the bins are shallow; 1024 when it does not, or when the bins are deep (F per bin
-        // at the 32x32 bin granularity as the depth proxy)
         const int rs = vertices ? FACE_REC : 9;
         g_last_fwd = LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
-                               (fuse && ntf == 256 && sh.C == MAXC ? NR_LAUNCH_STATIC_CHANNELS : 0)};
+                               (fuse && ntf == 256 && sh.C == MAXC ? NR_LAUNCH_STATIC_CHANNELS : 0) |
+                               (ordered ? NR_LAUNCH_DEEP_FIRST : 0)};
         if (fuse && ntf == 1024)
             hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order);
         else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
             hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order);
         else if (fuse)
             hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg);
+                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order);
         else if (ntf == 256)
             hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg);
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order);
         else
             hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg);
+                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra || fuse) return e;
@@ -399,13 +415,17 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     // k_vertex_grad's blocks also carry the texture-gradient output when that is a few texels per
     // thread; otherwise (no vertices, or a large texture) it gets a launch of its own
     constexpr int VB = 256;  // small blocks: more of them in flight for this latency-bound gather
-    const long long vgrad_threads = (nv + VB - 1) / VB * VB;
+    // items on XCDs (k_vertex_grad): a multiple of 8 items
+    const int xcd_items = a->batch_size % 8 == 0 && a->num_vertices > 0;
+    const long long vblocks = xcd_items ? (long long)a->batch_size * ((a->num_vertices + VB - 1) / VB) : (nv + VB - 1) / VB;
+    const long long vgrad_threads = vblocks * VB;
     const bool carry = nv > 0 && to.n <= 8 * vgrad_threads;
     if (nv > 0) {
         {
             ProfScope _p(P_VGRAD, st);
-            hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)((nv + VB - 1) / VB)), dim3(VB), 0, st, gF, a->vertex_offsets,
-                               a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv, carry ? to : TexOut{});
+            hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)vblocks), dim3(VB), 0, st, gF, a->vertex_offsets,
+                               a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv, carry ? to : TexOut{},
+                               xcd_items);
         }
         e = check_launch("k_vertex_grad");
         if (e) return e;

@@ -248,8 +248,9 @@ class _Cfg:
                  "tex_hw", "vt_shared", "Vt", "B", "tex_view")
 
 
-def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj=None, halo=None, light=None,
-          bg=None, tex4=None):
+def _args(cfg, vertices, faces, vt, ft, tex, fim):
+    """NrRasterArgs of one call: sizes, flags and the caller's tensors (the library's own buffers are
+    set from the arena layout, _Layout.fill)."""
     a = _lib.NrRasterArgs()
     a.batch_size = cfg.B
     a.num_vertices = cfg.V
@@ -264,19 +265,7 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj
     a.depth_min_delta = 1e-4
     a.vertices = vertices.data_ptr()
     a.faces = faces.data_ptr()
-    a.face_records = face_records.data_ptr()
     a.face_index = fim.data_ptr()
-    if ws is not None:
-        a.workspace = ws.data_ptr()
-        a.workspace_bytes = ws.numel()
-    else:  # the backward does not use the forward workspace
-        a.workspace = None
-        a.workspace_bytes = 0
-    if halo is not None:
-        a.halo = halo.data_ptr()
-    if adj is not None:
-        a.vertex_offsets = adj[0].data_ptr()
-        a.vertex_faces = adj[1].data_ptr()
     if cfg.flags & _lib.NR_DRAW_RGB:
         a.vertices_textures = vt.data_ptr()
         a.vt_batch_stride = vt.stride(0)
@@ -286,17 +275,6 @@ def _args(cfg, vertices, faces, vt, ft, tex, face_records, face_uv, fim, ws, adj
         a.textures = tex.data_ptr() + 4 * tv[0]
         a.tex_stride_b, a.tex_stride_c, a.tex_stride_p = tv[1], tv[2], tv[3]
         a.tex_height, a.tex_width = cfg.tex_hw
-        a.face_uv = face_uv.data_ptr()
-        if light is not None:  # (records, face_normals, vertex_normals, normal CSR offsets, faces)
-            a.num_lights = light[0].shape[0]
-            a.lights, a.face_normals, a.vertex_normals = light[0].data_ptr(), light[1].data_ptr(), light[2].data_ptr()
-            a.normal_offsets, a.normal_faces = light[3].data_ptr(), light[4].data_ptr()
-        if bg is not None:  # (backgrounds [B, 3, S, S] x-contiguous, grad_backgrounds or None)
-            a.backgrounds = bg[0].data_ptr()
-            a.bg_stride_b, a.bg_stride_c, a.bg_stride_y = bg[0].stride(0), bg[0].stride(1), bg[0].stride(2)
-            a.grad_backgrounds = bg[1].data_ptr() if bg[1] is not None else None
-        if tex4 is not None:  # RGBA-packed texels (NrRasterArgs.textures_packed)
-            a.textures_packed = tex4.data_ptr()
     return a
 
 
@@ -319,6 +297,86 @@ _BWD_PREZERO = os.environ.get("NR_BWD_PREZERO", "1") != "0"
 # no_grad) still allocates and zero-fills the workspace, and holds it as long as its graph lives.
 _BWD_PREZERO_MAX = 32 << 20
 _TEX_PACK_MAX_BYTES = 1 << 31
+
+
+def _align(n):
+    return (n + 255) & ~255
+
+
+class _Layout:
+    """The library's per-call buffers as byte offsets into ONE device allocation (the arena): face
+    records, face uv records, the forward's bin workspace, the halo cache, the packed texels, the
+    backward's pre-zeroed workspace and the light scratch.  The library takes raw pointers, so none of
+    them needs a tensor of its own: one caching-allocator call per forward instead of up to eight.
+    Computed once per configuration (sizes only) and cached."""
+    __slots__ = ("nbytes", "frec", "fuv", "ws", "ws_bytes", "halo", "halo_bytes", "tex4", "bws", "bws_bytes",
+                 "fnorm", "vnorm")
+
+    def __init__(self, L, cfg, uv_items, want_halo, want_bws, tex_grad, nl):
+        off = 0
+
+        def take(n):
+            nonlocal off
+            o = off
+            off += _align(n)
+            return o
+        B, F, V = cfg.B, cfg.F, cfg.V
+        S = cfg.image_size * (2 if cfg.aa else 1)
+        rgb = bool(cfg.flags & _lib.NR_DRAW_RGB)
+        self.frec = take(B * F * 16 * 4)
+        self.fuv = take(uv_items * F * 8 * 4) if rgb else None
+        self.ws_bytes = L.nr_workspace_bytes(B, F, S)
+        self.ws = take(self.ws_bytes)
+        self.halo = self.halo_bytes = None
+        if want_halo:
+            self.halo_bytes = L.nr_halo_bytes(B, cfg.image_size, int(cfg.aa), cfg.flags)
+            self.halo = take(self.halo_bytes)
+        self.tex4 = None
+        if rgb and _TEX_PACK:
+            H, W = cfg.tex_hw
+            n = L.nr_texture_packed_bytes(1 if cfg.tex_shared else B, H, W)
+            if n <= _TEX_PACK_MAX_BYTES:  # per-item atlases of hundreds of MB are sampled in place
+                self.tex4 = take(n)
+        self.bws = self.bws_bytes = None
+        if want_bws:
+            H, W = cfg.tex_hw
+            tex_items = (1 if cfg.tex_shared else B) if (rgb and tex_grad) else 0
+            n = L.nr_backward_workspace_bytes(B, F, V, tex_items, H, W, nl)
+            if n <= _BWD_PREZERO_MAX:
+                self.bws, self.bws_bytes = take(n), n
+        self.fnorm = self.vnorm = None
+        if nl:
+            self.fnorm, self.vnorm = take(B * F * 3 * 4), take(B * V * 4 * 4)
+        self.nbytes = max(off, 256)
+
+    def fill(self, a, base):
+        """Point the NrRasterArgs buffers at the arena at device address `base`."""
+        a.face_records = base + self.frec
+        if self.fuv is not None:
+            a.face_uv = base + self.fuv
+        a.workspace, a.workspace_bytes = base + self.ws, self.ws_bytes
+        if self.halo is not None:
+            a.halo = base + self.halo
+        if self.tex4 is not None:
+            a.textures_packed = base + self.tex4
+        if self.bws is not None:
+            a.bwd_workspace, a.bwd_workspace_bytes = base + self.bws, self.bws_bytes
+        if self.fnorm is not None:
+            a.face_normals, a.vertex_normals = base + self.fnorm, base + self.vnorm
+
+
+_layouts = {}
+
+
+def _layout(L, cfg, uv_items, want_halo, want_bws, tex_grad, nl):
+    key = (cfg.B, cfg.F, cfg.V, cfg.image_size, cfg.aa, cfg.flags, cfg.tex_hw, cfg.tex_shared, uv_items,
+           want_halo, want_bws, tex_grad, nl, _TEX_PACK)
+    lay = _layouts.get(key)
+    if lay is None:
+        if len(_layouts) > 64:
+            _layouts.clear()
+        lay = _layouts[key] = _Layout(L, cfg, uv_items, want_halo, want_bws, tex_grad, nl)
+    return lay
 
 
 class Rasterize(torch.autograd.Function):
@@ -345,55 +403,41 @@ class Rasterize(torch.autograd.Function):
             ctx.mark_non_differentiable(fim)
             ctx.set_materialize_grads(False)
             return torch.empty((0, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev), fim
-        fim = torch.empty((B, S, S), dtype=torch.int32, device=dev)
-        face_records = torch.empty((B, cfg.F, 16), dtype=torch.float32, device=dev)  # nr_raster.h NrRasterArgs
         rgb = bool(cfg.flags & _lib.NR_DRAW_RGB)
-        face_uv = None
-        if rgb:
-            uv_items = 1 if vertices_textures.stride(0) == 0 else B
-            face_uv = torch.empty((uv_items, cfg.F, 8), dtype=torch.float32, device=dev)
-        ws = torch.empty(L.nr_workspace_bytes(B, cfg.F, S), dtype=torch.uint8, device=dev)
+        grads = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        uv_items = (1 if vertices_textures.stride(0) == 0 else B) if rgb else 0
+        nl = light_recs.shape[0] if light_recs is not None else 0
+        lay = _layout(L, cfg, uv_items, _HALO_CACHE and grads, _BWD_PREZERO and grads,
+                      ctx.needs_input_grad[1], nl)
+        arena = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
+        fim = torch.empty((B, S, S), dtype=torch.int32, device=dev)
         images = torch.empty((B, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev)
-        # tile-border image values for the backward (nr_raster.h NrRasterArgs.halo), only when one will run
-        halo = None
-        if _HALO_CACHE and any(ctx.needs_input_grad[:2]):
-            halo = torch.empty(L.nr_halo_bytes(B, cfg.image_size, int(cfg.aa), cfg.flags) // 4, dtype=torch.float32,
-                               device=dev)
-            if _HALO_FILL is not None:
-                halo.fill_(_HALO_FILL)
+        a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, fim)
+        lay.fill(a, arena.data_ptr())
+        if _HALO_FILL is not None and lay.halo is not None:
+            arena[lay.halo:lay.halo + lay.halo_bytes].view(torch.float32).fill_(_HALO_FILL)
         light = None
         if light_recs is not None:
             nadj = _normal_adjacency(faces, cfg.V)
-            light = (light_recs, torch.empty((B, cfg.F, 3), dtype=torch.float32, device=dev),
-                     torch.empty((B, cfg.V, 4), dtype=torch.float32, device=dev), nadj[0], nadj[1])
-        bg = (backgrounds, None) if backgrounds is not None else None
-        tex4 = None
-        if rgb and _TEX_PACK:
-            H, W = cfg.tex_hw
-            nbytes = L.nr_texture_packed_bytes(1 if cfg.tex_shared else B, H, W)
-            if nbytes <= _TEX_PACK_MAX_BYTES:  # per-item atlases of hundreds of MB are sampled in place
-                tex4 = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-        a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, face_records, face_uv, fim, ws,
-                  halo=halo, light=light, bg=bg, tex4=tex4)
-        # the backward's workspace, allocated now so that the forward's setup launch zeroes its
-        # accumulators (NrRasterArgs.bwd_workspace): the backward then has no zero fill of its own
-        bws = None
-        if _BWD_PREZERO and any(ctx.needs_input_grad[:2]):
-            H, W = cfg.tex_hw
-            tex_items = (1 if cfg.tex_shared else B) if (rgb and ctx.needs_input_grad[1]) else 0
-            nl = light_recs.shape[0] if light_recs is not None else 0
-            nbytes = L.nr_backward_workspace_bytes(B, cfg.F, cfg.V, tex_items, H, W, nl)
-            if nbytes <= _BWD_PREZERO_MAX:
-                bws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-                a.bwd_workspace, a.bwd_workspace_bytes = bws.data_ptr(), bws.numel()
-        with torch.cuda.device(dev):
-            _lib.check(L.nr_rasterize_forward(a, _lib.ptr(images), _lib.stream_of(vertices)), "nr_rasterize_forward")
-        ctx.bws = bws  # zeroed for the first backward only (its accumulators are spent after it)
+            a.num_lights = nl
+            a.lights = light_recs.data_ptr()
+            a.normal_offsets, a.normal_faces = nadj[0].data_ptr(), nadj[1].data_ptr()
+            light = (light_recs, nadj)  # keeps the CSR alive as long as the graph
+        if backgrounds is not None and rgb:  # [B, 3, S, S] x-contiguous
+            a.backgrounds = backgrounds.data_ptr()
+            a.bg_stride_b, a.bg_stride_c, a.bg_stride_y = backgrounds.stride(0), backgrounds.stride(1), \
+                backgrounds.stride(2)
+        with _lib.on_device(dev):
+            _lib.check(L.nr_rasterize_forward(a, images.data_ptr(), _lib.stream_of(vertices)), "nr_rasterize_forward")
+        # the backward's workspace was zeroed by the setup launch (NrRasterArgs.bwd_workspace): for the
+        # first backward only (its accumulators are spent after it)
+        ctx.prezeroed = lay.bws is not None
+        ctx.arena = arena
+        ctx.layout = lay
+        ctx.args = a
         ctx.cfg = cfg
         ctx.light = light
-        ctx.tex4 = tex4
-        ctx.save_for_backward(vertices, textures, vertices_textures, faces, faces_textures, face_records, face_uv,
-                              fim, halo, backgrounds)
+        ctx.save_for_backward(vertices, textures, vertices_textures, faces, faces_textures, fim, backgrounds)
         ctx.mark_non_differentiable(fim)
         # no zero-filled gradient for the int32 face-index output (a 67 MB fill per backward at the
         # headline size otherwise)
@@ -409,59 +453,64 @@ class Rasterize(torch.autograd.Function):
             z = (lambda shp, i: torch.zeros(shp, dtype=torch.float32, device=dev) if ctx.needs_input_grad[i] else None)
             return (z((0, cfg.V, 3), 0), z(tshape, 1), z(vtshape, 2), None, None,
                     z(bshape, 5) if bshape is not None else None, z(lshape, 6) if lshape is not None else None, None)
-        vertices, textures, vt, faces, ft, face_records, face_uv, fim, halo, backgrounds = ctx.saved_tensors
-        if vt.ndim == 3 and vt.shape[0] == 1 and cfg.B > 1:
-            vt = vt.expand(cfg.B, -1, -1)
         if grad_images is None:
             return None, None, None, None, None, None, None, None
+        vertices, textures, vt, faces, ft, fim, backgrounds = ctx.saved_tensors
         grad_images = grad_images.contiguous()
         L = _lib.lib()
         dev = vertices.device
+        a = ctx.args  # the forward's arguments: same inputs and arena (the forward has consumed them)
+        a.workspace, a.workspace_bytes = None, 0  # the backward does not use the forward's bin workspace
         gv = torch.empty_like(vertices)
         gt = None
-        want_tex = bool(cfg.flags & _lib.NR_DRAW_RGB) and ctx.needs_input_grad[1]
+        rgb = bool(cfg.flags & _lib.NR_DRAW_RGB)
+        want_tex = rgb and ctx.needs_input_grad[1]
         tex_items = 0
+        H, W = cfg.tex_hw
         if want_tex:
-            H, W = cfg.tex_hw
             tex_items = 1 if cfg.tex_shared else cfg.B
             gt = torch.empty((tex_items, 3, H, W), dtype=torch.float32, device=dev)
-        H, W = cfg.tex_hw
         nl = ctx.light[0].shape[0] if ctx.light is not None else 0
         need = L.nr_backward_workspace_bytes(cfg.B, cfg.F, cfg.V, tex_items, H, W, nl)
-        prezeroed = ctx.bws is not None and ctx.bws.numel() == need
-        ws = ctx.bws if prezeroed else torch.empty(need, dtype=torch.uint8, device=dev)
-        ctx.bws = None
+        lay = ctx.layout
+        prezeroed = ctx.prezeroed and lay.bws_bytes == need
+        ctx.prezeroed = False
+        if prezeroed:
+            ws_ptr = a.bwd_workspace  # the library checks it is the buffer the forward zeroed
+            ws = None
+        else:
+            ws = torch.empty(need, dtype=torch.uint8, device=dev)
+            ws_ptr = ws.data_ptr()
         adj = _vertex_adjacency(faces, cfg.V)
+        a.vertex_offsets, a.vertex_faces = adj[0].data_ptr(), adj[1].data_ptr()
         gbg = None
-        if backgrounds is not None and ctx.needs_input_grad[5]:
-            gbg = torch.empty((cfg.B, 3) + tuple(backgrounds.shape[2:]), dtype=torch.float32, device=dev)
-        bg = (backgrounds, gbg) if backgrounds is not None else None
-        a = _args(cfg, vertices, faces, vt, ft, textures, face_records, face_uv, fim, None, adj, halo, ctx.light, bg,
-                  tex4=ctx.tex4)
-        if prezeroed:  # the library checks that the workspace it may skip zeroing is the one the forward zeroed
-            a.bwd_workspace, a.bwd_workspace_bytes = ws.data_ptr(), ws.numel()
-        with torch.cuda.device(dev):
+        if backgrounds is not None and rgb:
+            if ctx.needs_input_grad[5]:
+                gbg = torch.empty((cfg.B, 3) + tuple(backgrounds.shape[2:]), dtype=torch.float32, device=dev)
+            a.grad_backgrounds = gbg.data_ptr() if gbg is not None else None
+        stream = _lib.stream_of(vertices)
+        with _lib.on_device(dev):
             # workspace_zeroed = 1 only for the first backward after the forward zeroed it (no fill)
-            _lib.check(L.nr_rasterize_backward(a, _lib.ptr(grad_images), _lib.ptr(gv), _lib.ptr(gt), _lib.ptr(ws),
-                                               ws.numel(), int(prezeroed), _lib.stream_of(vertices)),
-                       "nr_rasterize_backward")
+            _lib.check(L.nr_rasterize_backward(a, grad_images.data_ptr(), gv.data_ptr(),
+                                               gt.data_ptr() if gt is not None else None, ws_ptr, need,
+                                               int(prezeroed), stream), "nr_rasterize_backward")
         if gt is not None:
             # the Function's texture input is [B, 3, H, W], or the single [3, H, W] / [1, 3, H, W]
             # source of a shared texture (see rasterize_core): same element count as gt either way
             gt = gt.reshape(textures.shape)
         # vertices_textures and light parameters (rasterize.py:246, 252-283): a second, separate pass
         gvt = glt = None
-        want_vt = bool(cfg.flags & _lib.NR_DRAW_RGB) and ctx.needs_input_grad[2]
-        want_lt = bool(cfg.flags & _lib.NR_DRAW_RGB) and ctx.needs_input_grad[6] and ctx.light is not None
+        want_vt = rgb and ctx.needs_input_grad[2]
+        want_lt = rgb and ctx.needs_input_grad[6] and ctx.light is not None
         if want_vt or want_lt:
             if want_vt:
                 # the Function's vt input is [B, Vt, 2] per item, or the [1, Vt, 2] source of a shared one
                 gvt = torch.empty(tuple(ctx.vt_shape), dtype=torch.float32, device=dev)
             if want_lt:
                 glt = torch.empty_like(ctx.light[0])
-            with torch.cuda.device(dev):
-                _lib.check(L.nr_rasterize_backward_params(a, _lib.ptr(grad_images), _lib.ptr(gvt), _lib.ptr(glt),
-                                                          _lib.stream_of(vertices)), "nr_rasterize_backward_params")
+            with _lib.on_device(dev):
+                _lib.check(L.nr_rasterize_backward_params(a, grad_images.data_ptr(), _lib.ptr(gvt), _lib.ptr(glt),
+                                                          stream), "nr_rasterize_backward_params")
         return (gv if ctx.needs_input_grad[0] else None), gt, gvt, None, None, gbg, glt, None
 
 

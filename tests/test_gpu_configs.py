@@ -120,7 +120,7 @@ def test_cfg3_car_subdivided_vs_oracle(oracle_mod, dev):
     map bit-exact, images, vertex gradients.  A second backward of the same graph with the upstream
     gradient kept on those 16 items only gives the shared atlas gradient, checked against the
     oracle's sum over them (rasterize.py:144-148 scatter).  The deep bins take the 1024-thread
-    forward (asserted from the library's launch record)."""
+    forward, dispatched deepest bin first (asserted from the library's launch record)."""
     v, f, vt, ft, tex = nr.load_obj(CAR, load_textures=True)
     v, f, vt, ft = synthetic.subdivide(v, f, vt, ft)
     assert f.shape[0] == 14576
@@ -135,7 +135,7 @@ def test_cfg3_car_subdivided_vs_oracle(oracle_mod, dev):
     pv = proj.to(dev).requires_grad_(True)
     img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, hp, return_face_index=True)
     assert img.shape == (B, 4, s, s)
-    assert _lib.last_launch("k_raster_fwd") == (1024, _lib.NR_LAUNCH_FUSED_SHADE)
+    assert _lib.last_launch("k_raster_fwd") == (1024, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_DEEP_FIRST)
     counts = _bin_candidates(proj[:4], f, 2 * s)
     assert counts.max() > 512, counts.max()  # deep bins: more than one 512-face staging round
     g = torch.randn(img.shape, generator=torch.Generator().manual_seed(43))

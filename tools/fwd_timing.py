@@ -46,10 +46,10 @@ from neural_renderer_v2_pytorch_amd import _lib  # noqa: E402
 L = _lib.lib()
 S = 2 * size
 blocks = (S // 32) ** 2 * batch
-n = blocks * waves * 8
+n = blocks * waves * 10
 buf = (ctypes.c_ulonglong * n)()
 assert L.nr_debug_fwd_timing(buf, ctypes.c_size_t(n)) == 0
-t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(blocks, waves, 8)
+t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(blocks, waves, 10)
 nc = t[:, 0, 6]
 st = t[:, :, 2]  # cycles in the staging rounds (face loads + LDS stores + barrier), summed
 ph = np.stack([t[:, :, 1] - t[:, :, 0], st, t[:, :, 3] - t[:, :, 1] - st,
@@ -69,3 +69,26 @@ for lo, hi, lab in ((0, 0, "no candidates"), (1, 10**9, "with candidates")):
     for i, nm in enumerate(names):
         x = ph[sel][:, :, i].ravel()
         print("   %-9s mean %8.0f  p50 %8.0f  p90 %8.0f" % (nm, x.mean(), *np.percentile(x, [50, 90])))
+
+# where the kernel's wave time goes, by the bin's candidate count: share of the summed wave lifetimes
+# (what the chip spends), and the walk's mean per wave
+tot = life.sum()
+print("wave-time share by candidates per bin (and walk mean per wave):")
+for lo, hi in ((0, 0), (1, 64), (65, 160), (161, 512), (513, 2048), (2049, 10**9)):
+    sel = (nc >= lo) & (nc <= hi)
+    if sel.any():
+        print("   %5d-%-9d bins %6d  time share %5.1f%%  walk mean %9.0f  lifetime mean %9.0f" % (
+            lo, min(hi, 10**6), sel.sum(), 100 * life[sel].sum() / tot, ph[sel][:, :, 2].mean(), life[sel].mean()))
+
+# timeline from the chip-wide wall clock (100 MHz): when the bins of each depth class start and end,
+# relative to the kernel's first wave (the kernel ends with its last block)
+ws_, we_ = t[:, :, 8].min(1), t[:, :, 9].max(1)
+t0 = ws_.min()
+span = (we_.max() - t0) / 100.0
+print("kernel span %.1f us (wall clock)" % span)
+for lo, hi in ((0, 0), (1, 160), (161, 512), (513, 2048), (2049, 10**9)):
+    sel = (nc >= lo) & (nc <= hi)
+    if sel.any():
+        st_, en_ = (ws_[sel] - t0) / 100.0, (we_[sel] - t0) / 100.0
+        print("   %5d-%-9d start mean %7.1f max %7.1f us   end mean %7.1f max %7.1f us   duration mean %6.1f max %6.1f us" % (
+            lo, min(hi, 10**6), st_.mean(), st_.max(), en_.mean(), en_.max(), (en_ - st_).mean(), (en_ - st_).max()))

@@ -89,6 +89,35 @@ def main():
         params()
         nr.RasterizeHyperparam(image_size=s)
 
+    # time spent inside Rasterize.forward / backward (the backward runs on torch's autograd device
+    # thread) and inside the library's launch calls, per step
+    acc = {}
+
+    def timed(name, fn):
+        def w(*a, **k):
+            t0 = time.perf_counter()
+            r = fn(*a, **k)
+            acc[name] = acc.get(name, 0.0) + time.perf_counter() - t0
+            return r
+        return w
+    fwd0, bwd0 = nrr.Rasterize.forward, nrr.Rasterize.backward
+    nrr.Rasterize.forward = staticmethod(timed("Rasterize.forward", fwd0))
+    nrr.Rasterize.backward = staticmethod(timed("Rasterize.backward", bwd0))
+    orig = {fname: getattr(L, fname) for fname in ("nr_rasterize_forward", "nr_rasterize_backward")}
+    for fname, f0 in orig.items():
+        setattr(L, fname, timed(fname, f0))
+    core0 = nrr.rasterize_core
+    nr.rasterize_core = timed("rasterize_core", core0)
+    h, a = per_call_us(step)
+    n = N + 20
+    print("instrumented step: host %.1f us/call" % h)
+    for k, v in sorted(acc.items()):
+        print("  %-28s %8.1f us/step" % (k, 1e6 * v / n))
+    nrr.Rasterize.forward, nrr.Rasterize.backward = staticmethod(fwd0), staticmethod(bwd0)
+    nr.rasterize_core = core0
+    for fname, f0 in orig.items():
+        setattr(L, fname, f0)  # back to the configured function objects (argtypes / restype)
+
     for name, fn in [("step", step), ("forward (grad on)", fwd_grad), ("forward (no_grad)", fwd_nograd),
                      ("tiny autograd fwd+bwd", tiny_autograd), ("ctypes call", ctypes_call),
                      ("8 x torch.empty", empties), ("RasterizeParam + Hyperparam", params_only)]:

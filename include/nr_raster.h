@@ -56,9 +56,10 @@ NR_API int nr_version(void);
 /* sizeof(NrRasterArgs), for bindings to check their mirror of the struct */
 NR_API size_t nr_raster_args_size(void);
 
-/* ABI version of this header: 4 (nr_last_launch added; 3: workspace_zeroed of nr_rasterize_backward).
+/* ABI version of this header: 5 (NrRasterArgs.face_index_sparse; 4: nr_last_launch; 3: workspace_zeroed of
+ * nr_rasterize_backward).
  * Bindings check it, and nr_raster_args_size(), before the first call. */
-#define NR_ABI_VERSION 4
+#define NR_ABI_VERSION 5
 
 /* Scratch bytes needed by the face-index map for B items, F faces, S x S internal pixels
  * (per-face screen bounding boxes + coarse-bin face bitmasks). */
@@ -160,6 +161,12 @@ typedef struct NrRasterArgs {
      * workspace next (after a backward its accumulators are no longer zero).  NULL = nothing zeroed. */
     void* bwd_workspace;
     size_t bwd_workspace_bytes;
+    /* 1 = the caller reads face_index only inside the 32x32 bins that hold candidate faces (the
+     * backward with a halo cache reads no other entry; a bin without candidates is -1 throughout): the
+     * fused forward then leaves those bins' -1 entries unwritten (64 % of the headline's face-index
+     * map).  Honoured only with the halo cache and the fused shading; nr_rasterize_backward_params
+     * (which reads every entry) refuses such a forward state.  0 = face_index fully written. */
+    int face_index_sparse;
 } NrRasterArgs;
 
 enum { NR_LIGHT_AMBIENT = 0, NR_LIGHT_DIRECTIONAL = 1, NR_LIGHT_SPECULAR = 2, NR_LIGHT_FLOATS = 8 };

@@ -28,7 +28,7 @@ EXPORTS = [
     "nr_last_launch",
 ]
 
-ABI_VERSION = 4  # include/nr_raster.h NR_ABI_VERSION
+ABI_VERSION = 5  # include/nr_raster.h NR_ABI_VERSION
 
 NR_LAUNCH_FUSED_SHADE, NR_LAUNCH_STATIC_CHANNELS, NR_LAUNCH_TWO_PX_PER_LANE, NR_LAUNCH_DEEP_FIRST = 1, 2, 4, 8
 
@@ -52,7 +52,7 @@ class NrRasterArgs(ctypes.Structure):
         ("normal_offsets", c_void_p), ("normal_faces", c_void_p),
         ("backgrounds", c_void_p), ("bg_stride_b", c_ll), ("bg_stride_c", c_ll), ("bg_stride_y", c_ll),
         ("grad_backgrounds", c_void_p), ("textures_packed", c_void_p),
-        ("bwd_workspace", c_void_p), ("bwd_workspace_bytes", c_size_t),
+        ("bwd_workspace", c_void_p), ("bwd_workspace_bytes", c_size_t), ("face_index_sparse", c_int),
     ]
 
 NR_LIGHT_AMBIENT, NR_LIGHT_DIRECTIONAL, NR_LIGHT_SPECULAR, NR_LIGHT_FLOATS = 0, 1, 2, 8

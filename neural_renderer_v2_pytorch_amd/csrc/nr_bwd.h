@@ -709,7 +709,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                 if (LIT) an += on ? rw * rn : 0.f;  // corner-normal gradient tt = 3 corner + axis
             };
             // one loop over both pixel rows (2- and 4-member steps measured slower)
+#ifndef NR_ABL_NOGATHER  // timing builds only: no member loop
             for (; mine; mine &= mine - 1) member(rbase + __builtin_ctz(mine) * REC, true);
+#else
+            (void)rbase;
+#endif
         }
         // reduce-scatter over the 4 member chunks (lanes t, t+16, t+32, t+48) with the gfx950 lane
         // swaps (VALU, no LDS round trip): lane (t, c) ends with the chunk total of value c
@@ -732,7 +736,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             const bool face_lane = chunk == 3 && tt < 9;
             const float fv = face_lane ? v : pend;
             float* dst = tex_lane ? gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk : gFb + key * 9 + tt;
+#ifdef NR_ABL_NOATOM  // timing builds only: no flush atomics
+            if ((tex_lane || face_lane) && fv == 12345.f) unsafeAtomicAdd(dst, fv);
+#else
             if ((tex_lane || face_lane) && fv != 0.f) unsafeAtomicAdd(dst, fv);
+#endif
             if (win) {
                 pend = sw ? v : pend + v;
                 pwx = wx;

@@ -377,7 +377,12 @@ __device__ __forceinline__ void sample_texture(const Face& f, const float w[3], 
         const float4* t4b = tv.t4 + (long long)bt * tv.HWp;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
+#ifdef NR_ABL_NOTEX  // timing builds only: no texel loads (constant texels)
+            q4[i] = make_float4(0.25f * i, 0.5f, 0.75f, 0.f);
+            (void)t4b;
+#else
             q4[i] = t4b[s.idx[i]];
+#endif
         }
     } else {
 #pragma unroll

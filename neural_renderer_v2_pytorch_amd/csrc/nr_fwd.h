@@ -19,15 +19,27 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     const float* __restrict__ vt, long long vt_bstride, int Vt,
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
                                                     int uv_items, float* __restrict__ fnorm, TexPack pk, ZeroFill zf,
-                                                    int* __restrict__ bin_count) {
+                                                    int* __restrict__ bin_count, int xcd_items) {
     __shared__ int2 s_bb[SETUP_FACES];
     // the block's face records, assembled per face and then written out coalesced (a record per lane
     // would store 64-B strided rows); the bin-mask words reuse the space afterwards
     extern __shared__ __attribute__((aligned(16))) float s_stage[];  // setup_lds_words(nbins) floats
     float* s_frec = s_stage;
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_stage);
-    const int b = blockIdx.y;
-    const int f0 = blockIdx.x * SETUP_FACES;
+    // xcd_items (B % 8 == 0): block L works on item (L & 7) + 8 (j / groups), face group j % groups
+    // (j = L >> 3): workgroups are dealt to XCD L % 8, so all of an item's blocks write through one L2,
+    // where the 24-B pieces that neighbouring face groups write into each bin's mask row meet in whole
+    // lines before they go to HBM (spread over eight L2s, each piece went out as a partial line)
+    int b, grp;
+    if (xcd_items) {
+        const int L = blockIdx.y * gridDim.x + blockIdx.x, j = L >> 3;
+        b = (L & 7) + 8 * (j / gridDim.x);
+        grp = j % gridDim.x;
+    } else {
+        b = blockIdx.y;
+        grp = blockIdx.x;
+    }
+    const int f0 = grp * SETUP_FACES;
     const int t = threadIdx.x;
     if (pk.out && t >= SETUP_FACES) {  // the threads the face phase leaves idle repack the textures
         long long lo, hi;
@@ -124,7 +136,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         __syncthreads();
     }
     // coarse-bin bitmask words of this face group
-    const int w0 = blockIdx.x * (SETUP_FACES / 32);
+    const int w0 = grp * (SETUP_FACES / 32);
     const int nw = min(SETUP_FACES / 32, nwords - w0);
     if (nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS) {  // (setup_lds_words sized s_stage for this)
         // each face sets its bit in the (few) bins its pixel range touches (LDS ds_or), then the
@@ -474,7 +486,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                                                   int F, Geom g, float near, float far, float delta,
                                                   int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
                                                   float* __restrict__ halo, uint8_t* __restrict__ binfg,
-                                                  const int* __restrict__ order) {
+                                                  const int* __restrict__ order, int fim_sparse) {
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
@@ -521,7 +533,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     if (dyn) {
         ncand = total0;
         if (ncand == 0) {
-            for (int u = wid; u < 16; u += C::NW) {
+            for (int u = wid; u < 16 && !fim_sparse; u += C::NW) {
                 const int px = bx0 + (u & 3) * 8 + (lane & 7), py = by0 + (u >> 2) * 8 + (lane >> 3);
                 if (px < S && py < S) fimb[(int)__umul24(py, S) + px] = -1;
             }
@@ -628,7 +640,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
             int ox, oy;
             C::block_of(wid, k, ox, oy);
             const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
-            if (px < S && py < S) fimb[(int)__umul24(py, S) + px] = best[k];
+            if (px < S && py < S && (ncand > 0 || !fim_sparse)) fimb[(int)__umul24(py, S) + px] = best[k];
         }
         if (SHADE && ncand > 0) {
             // the bin's 32x32 face ids go through LDS (the staging area is free once every wave has walked)

@@ -67,7 +67,7 @@ __global__ void k_selftest_div(const float* __restrict__ a, const float* __restr
 extern "C" {
 
 const char* nr_last_error(void) { return g_err.c_str(); }
-int nr_version(void) { return 4; }
+int nr_version(void) { return 5; }
 size_t nr_raster_args_size(void) { return sizeof(NrRasterArgs); }
 
 int nr_num_channels(int draw_flags) {
@@ -128,11 +128,11 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
                                rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk, zf,
-                               ordered ? bin_count : nullptr);
+                               ordered ? bin_count : nullptr, B % 8 == 0);
         else
             hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
-                               nullptr, pk, zf, ordered ? bin_count : nullptr);
+                               nullptr, pk, zf, ordered ? bin_count : nullptr, B % 8 == 0);
         int e = check_launch("k_face_setup");
         if (e) return e;
         if (lit && V > 0) {
@@ -156,6 +156,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     const bool fuse = ra && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
     // per-bin foreground flags after the halo values (the backward skips background tiles)
     uint8_t* binfg = (ra && ra->halo) ? (uint8_t*)ra->halo + halo_flags_offset_bytes(B, S, sh.C) : nullptr;
+    // empty bins leave their -1 face ids unwritten (NrRasterArgs.face_index_sparse): with the fused
+    // shading nothing else in this launch reads them, and the backward skips those tiles by the flags
+    const int sparse = (ra && ra->face_index_sparse && fuse && binfg) ? 1 : 0;
     {
         ProfScope _p(P_RASTER, st);
         const int rs = vertices ? FACE_REC : 9;
@@ -164,19 +167,19 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                (ordered ? NR_LAUNCH_DEEP_FIRST : 0)};
         if (fuse && ntf == 1024)
             hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse);
         else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
             hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse);
         else if (fuse)
             hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order);
+                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse);
         else if (ntf == 256)
             hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order);
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0);
         else
             hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order);
+                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra || fuse) return e;
@@ -447,6 +450,8 @@ int nr_rasterize_backward_params(const NrRasterArgs* a, const float* grad_images
     const bool rgb = (a->draw_flags & NR_DRAW_RGB) != 0;
     const bool uv = rgb && grad_vertices_textures, lgt = rgb && grad_lights && a->num_lights > 0;
     if ((grad_vertices_textures || grad_lights) && !rgb) return fail(NR_ERR_ARGS, "parameter gradients need NR_DRAW_RGB");
+    if (a->face_index_sparse && (grad_vertices_textures || grad_lights))
+        return fail(NR_ERR_ARGS, "parameter gradients read every face id: the forward must not use face_index_sparse");
     if (grad_lights && a->num_lights > 0 && !a->vertex_normals) return fail(NR_ERR_ARGS, "lights need vertex_normals");
     hipStream_t st = (hipStream_t)stream;
     const int B = a->batch_size;

@@ -245,7 +245,7 @@ def _light_records(lights, B, dev):
 
 class _Cfg:
     __slots__ = ("image_size", "aa", "backside", "flags", "near", "far", "eps", "C", "V", "F", "tex_shared",
-                 "tex_hw", "vt_shared", "Vt", "B", "tex_view")
+                 "tex_hw", "vt_shared", "Vt", "B", "tex_view", "want_fim")
 
 
 def _args(cfg, vertices, faces, vt, ft, tex, fim):
@@ -284,6 +284,10 @@ _HALO_CACHE = os.environ.get("NR_HALO_CACHE", "1") != "0"
 # test hook: a value the halo cache is filled with before the forward (NaN in the parity tests, which
 # so check that the backward reads only values the forward wrote, or infers from the bin flags)
 _HALO_FILL = None
+# test hook: a face id the face-index map is filled with before the forward (a valid id in the parity
+# tests, so that a backward reading an entry the sparse forward left unwritten would show up in the
+# gradients)
+_FIM_FILL = None
 # the forward packs the texels into RGBA rows that forward and backward sample (NrRasterArgs.
 # textures_packed); False samples the [B, 3, H, W] textures directly (same results)
 _TEX_PACK = os.environ.get("NR_TEX_PACK", "1") != "0"
@@ -414,6 +418,8 @@ class Rasterize(torch.autograd.Function):
         images = torch.empty((B, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev)
         a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, fim)
         lay.fill(a, arena.data_ptr())
+        if _FIM_FILL is not None:
+            fim.fill_(_FIM_FILL)
         if _HALO_FILL is not None and lay.halo is not None:
             arena[lay.halo:lay.halo + lay.halo_bytes].view(torch.float32).fill_(_HALO_FILL)
         light = None
@@ -427,6 +433,11 @@ class Rasterize(torch.autograd.Function):
             a.backgrounds = backgrounds.data_ptr()
             a.bg_stride_b, a.bg_stride_c, a.bg_stride_y = backgrounds.stride(0), backgrounds.stride(1), \
                 backgrounds.stride(2)
+        # the face-index map stays internal (not returned) and only the backward reads it, through the
+        # halo cache's bin flags: empty bins need not write their -1 entries (NrRasterArgs.
+        # face_index_sparse).  Not when the parameter-gradient pass (vertices_textures) reads them all.
+        a.face_index_sparse = int(lay.halo is not None and not cfg.want_fim and backgrounds is None and
+                                  light_recs is None and not (rgb and ctx.needs_input_grad[2]))
         with _lib.on_device(dev):
             _lib.check(L.nr_rasterize_forward(a, images.data_ptr(), _lib.stream_of(vertices)), "nr_rasterize_forward")
         # the backward's workspace was zeroed by the setup launch (NrRasterArgs.bwd_workspace): for the
@@ -561,6 +572,7 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
     cfg.flags = flags
     cfg.near, cfg.far, cfg.eps = float(hyperparams.near), float(hyperparams.far), float(hyperparams.eps)
     cfg.C = _lib.lib().nr_num_channels(flags)
+    cfg.want_fim = bool(return_face_index)
     fi = _faces_i32(faces_t, dev, cfg.V, "faces")
     tex = vt = ft = None
     cfg.tex_shared = cfg.vt_shared = False

@@ -422,6 +422,44 @@ def test_headline_full_batch_vs_oracle(oracle_mod, dev):
     close_grads(leaf.grad, rgt, "shared texture gradient (sum over 64 items)")
 
 
+def test_sparse_face_index_forward_vs_oracle(oracle_mod, dev):
+    """The forward whose face-index map stays internal (return_face_index=False, halo cache on)
+    leaves the -1 entries of bins without candidate faces unwritten (NrRasterArgs.face_index_sparse);
+    the backward must read none of them.  The map is filled with face id 0 before the forward, so a
+    read of an unwritten entry would add face 0's gradient at a background pixel: images and
+    gradients of 8 headline items (ico 5120, 256^2 AA, rgb + sil + depth, shared texture) against
+    the oracle, and against the same render with the full map (return_face_index=True)."""
+    B = 8
+    proj, f = _ico_batch(4, B, dev)
+    vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
+    tex_cpu = torch.rand(tex.shape, generator=torch.Generator().manual_seed(5))
+    g = torch.randn((B, 5, 256, 256), generator=torch.Generator().manual_seed(6))
+    out = {}
+    for want_fim in (False, True):
+        leaf = tex_cpu.to(dev).requires_grad_(True)
+        pv = proj.to(dev).requires_grad_(True)
+        params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                                   faces_textures=torch.as_tensor(ft, device=dev),
+                                   textures=leaf[None].expand(B, -1, -1, -1))
+        nrr._FIM_FILL = 0
+        try:
+            img = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, nr.RasterizeHyperparam(),
+                                     return_face_index=want_fim)
+        finally:
+            nrr._FIM_FILL = None
+        if want_fim:
+            img = img[0]
+        img.backward(g.to(dev))
+        out[want_fim] = (img.detach(), pv.grad, leaf.grad)
+    assert torch.equal(out[False][0], out[True][0])
+    ref, rfim, rgv, rgt = oracle_batch(oracle_mod, proj, f, g, 256, tex_cpu, vt, ft)
+    assert int((rfim < 0).sum()) > 0.5 * rfim.size  # most of the map is background
+    for k in (False, True):
+        close_images(out[k][0], ref, "images (full map %d)" % k)
+        close_grads(out[k][1], rgv, "grad vertices (full map %d)" % k)
+        close_grads(out[k][2], rgt, "grad textures (full map %d)" % k)
+
+
 def test_tiny_depth_faces_vs_oracle(oracle_mod, dev):
     """Faces whose z + 1e-10 does not round to z (FACE_ZQ_EQ clear: the texture sampling divides by
     z + 1e-10 itself) beside faces where it does (the depth's w / z terms are reused), mixed within

@@ -200,11 +200,18 @@ def main():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--loop-steps", type=int, default=200)
     p.add_argument("--only", default="cfg2,cfg3,cfg5")
+    p.add_argument("--calibrate", action="store_true",
+                   help="end with bench.py's 1 GiB copy stream (the FETCH_SIZE / WRITE_SIZE calibration of "
+                        "tools/pmc_traffic.py when this runs under rocprofv3 --pmc)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     for name in a.only.split(","):
         r = globals()[name](dev, a)
         print(json.dumps(r), flush=True)
+    if a.calibrate:
+        import bench
+        torch.cuda.synchronize()
+        print(json.dumps({"copy_ceiling_gbs": round(bench.copy_ceiling_gbs(dev), 1)}), flush=True)
 
 
 if __name__ == "__main__":

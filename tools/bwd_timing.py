@@ -1,6 +1,7 @@
-"""Per-wave phase timing of k_raster_bwd on the headline workload (timing build, NR_BWD_TIMING).
+"""Per-wave phase timing of k_raster_bwd on the headline workload or the car (--workload car, BASELINE
+cfg3) (timing build, NR_BWD_TIMING).
 
-usage (GPU box): python tools/bwd_timing.py [extra -D flags...]
+usage (GPU box): python tools/bwd_timing.py [--workload car] [extra -D flags...]
 Builds the library with -DNR_BWD_TIMING into /tmp, runs bench.py's headline step through it, reads
 the per-wave shader-clock stamps of the last backward (nr_debug_bwd_timing) and prints the mean and
 percentiles of each phase: step 1 (recompute + staging of I and G), barrier 1, stencil, barrier 2,
@@ -14,6 +15,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 lib_path = "/tmp/libnr_timing.so"
+WORKLOAD = "headline"
+if len(sys.argv) > 2 and sys.argv[1] == "--workload":
+    WORKLOAD = sys.argv[2]
+    del sys.argv[1:3]
 sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402  (the product's hipcc flags)
 subprocess.check_call(["/opt/rocm/bin/hipcc", *__graft_entry__.hipcc_flags(), "-DNR_BWD_TIMING", "-I" + ROOT + "/include"]
@@ -24,16 +29,25 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 sys.argv = [sys.argv[0]]
-args = bench.parse()
 torch.cuda.set_device(0)
-w = bench.workload(args, 0, torch.device("cuda", 0))
+if WORKLOAD == "car":  # BASELINE cfg3 (tools/bench_configs.py)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs  # noqa: E402
+    step, _, batch, size = bench_configs.cfg3_step(torch.device("cuda", 0))
+else:
+    args = bench.parse()
+    w = bench.workload(args, 0, torch.device("cuda", 0))
+    batch, size = args.batch, args.image_size
+
+    def step():
+        bench.step(w)
 for _ in range(4):
-    bench.step(w)
+    step()
 torch.cuda.synchronize()
 from neural_renderer_v2_pytorch_amd import _lib  # noqa: E402
 L = _lib.lib()
-S = 2 * args.image_size
-blocks = (S // 32) * (S // 16) * args.batch
+S = 2 * size
+blocks = (S // 32) * (S // 16) * batch
 n = blocks * 4 * 8
 buf = (ctypes.c_ulonglong * n)()
 assert L.nr_debug_bwd_timing(buf, ctypes.c_size_t(n)) == 0

@@ -216,33 +216,69 @@ __global__ void k_vertex_normals(const float* __restrict__ fnorm, const int32_t*
 // bucket), longest first: one list per XCD when B is a multiple of 8 (list x: items = x mod 8, read by
 // the blocks dealt to XCD x, ordered_bin), else one list.  Any order gives the same results: every
 // bin's block is independent.
-__device__ __forceinline__ int count_bucket(int c) { return c <= 0 ? 0 : min(15, 32 - __clz(c)); }
+// buckets of the candidate count, deepest = highest: one per octave (0 for none)
+constexpr int ORDER_BUCKETS = 16;
+__device__ __forceinline__ int count_bucket(int c) { return c <= 0 ? 0 : min(ORDER_BUCKETS - 1, 32 - __clz(c)); }
+// one block of 1024 threads per list, a stable counting sort: each wave takes 64-entry chunks and counts
+// its chunk's buckets with ballots; the per-(chunk, bucket) counts become output offsets (deepest
+// bucket first, chunks in list order); each entry then goes to its chunk's offset plus its rank among
+// the chunk's lanes of the same bucket.  Stable: screen order (and so neighbouring bins, which share
+// face records in L2) within a bucket -- an unstable order cost the car's forward ~6 us.
+constexpr int ORDER_MAX_ENTRIES = 64 * 256;
 __global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt, int* __restrict__ order, int B,
                                                     int nbins) {
-    __shared__ int s_scan[16];
+    __shared__ int s_h[ORDER_MAX_ENTRIES / 64][ORDER_BUCKETS];
+    __shared__ int s_base[ORDER_BUCKETS];
     const bool per_xcd = gridDim.x == 8;
     const int x = blockIdx.x;
     const int items = per_xcd ? B / 8 : B;
     const int n = items * nbins;
-    const int c = (n + blockDim.x - 1) / blockDim.x;
-    const int lo = threadIdx.x * c, hi = min(lo + c, n);
+    const int nch = (n + 63) / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
     int* __restrict__ out = order + (per_xcd ? x * n : 0);
     auto entry = [&](int k) {
         const int j = k / nbins;
         return (per_xcd ? x + 8 * j : j) * nbins + (k - j * nbins);
     };
-    int base = 0;
-    for (int bk = 15; bk >= 0; bk--) {
-        int m = 0;
-        for (int k = lo; k < hi; k++) m += count_bucket(cnt[entry(k)]) == bk;
-        int tot;
-        int p = base + block_scan<16>(m, tot, s_scan);
-        if (m)
-            for (int k = lo; k < hi; k++) {
-                const int e = entry(k);
-                if (count_bucket(cnt[e]) == bk) out[p++] = e;
-            }
-        base += tot;
+    for (int ch = wid; ch < nch; ch += nw) {
+        const int k = ch * 64 + lane;
+        const int bk = k < n ? count_bucket(cnt[entry(k)]) : -1;
+#pragma unroll
+        for (int b = 0; b < ORDER_BUCKETS; b++) {
+            const int c = __popcll(__ballot(bk == b));
+            if (lane == 0) s_h[ch][b] = c;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < ORDER_BUCKETS) {  // bucket totals
+        int tot = 0;
+        for (int ch = 0; ch < nch; ch++) tot += s_h[ch][threadIdx.x];
+        s_base[threadIdx.x] = tot;
+    }
+    __syncthreads();
+    if (threadIdx.x < ORDER_BUCKETS) {  // this bucket's chunk offsets: buckets deepest first
+        const int b = threadIdx.x;
+        int base = 0;
+        for (int bb = ORDER_BUCKETS - 1; bb > b; bb--) base += s_base[bb];
+        for (int ch = 0; ch < nch; ch++) {
+            const int c = s_h[ch][b];
+            s_h[ch][b] = base;
+            base += c;
+        }
+    }
+    __syncthreads();
+    for (int ch = wid; ch < nch; ch += nw) {
+        const int k = ch * 64 + lane;
+        const int e = k < n ? entry(k) : 0;
+        const int bk = k < n ? count_bucket(cnt[e]) : -1;
+        int rank = 0;
+#pragma unroll
+        for (int b = 0; b < ORDER_BUCKETS; b++) {
+            const unsigned long long m = __ballot(bk == b);
+            if (bk == b) rank = __popcll(m & lt);
+        }
+        if (k < n) out[s_h[ch][bk] + rank] = e;
     }
 }
 

@@ -99,8 +99,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     const int ntf = (blocks >= 8192 && faces_per_bin < 40.0) ? 256 : 1024;
     // deep bins (the car, the 50k torus): dispatch the bins deepest first (k_bin_order), from candidate
     // counts the setup adds up (its LDS bin-mask path); a list per XCD needs B % 8 == 0 or fits one block
+    const long long order_list = (B % 8 == 0 ? B / 8 : B) * (long long)g.nbins;  // entries per k_bin_order block
     const bool ordered = F > 0 && ntf == 1024 && faces_per_bin >= 24.0 &&
-                         (long long)g.nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS;
+                         (long long)g.nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS && order_list <= ORDER_MAX_ENTRIES;
     if (ordered && hipMemsetAsync(bin_count, 0, (size_t)B * g.nbins * 4, st) != hipSuccess)
         return check_launch("hipMemsetAsync");
     // the setup's idle threads repack the textures when that takes them up to 32 texels each; with no

@@ -150,9 +150,18 @@ def _faces_i32(faces, device, bound, what):
     """[F,3] int32 on `device`, indices checked like the reference's IndexError on out-of-range
     indices (rasterize.py:232, :246).  CPU index tensors are checked on the host before the copy;
     device-resident int32 ones once per (storage, version), so steady-state calls never sync."""
-    f = torch.as_tensor(faces)
+    f = faces if isinstance(faces, torch.Tensor) else torch.as_tensor(faces)
     if f.ndim != 2 or f.shape[1] != 3:
         raise AssertionError("%s must be [F, 3]" % what)
+    if f.is_cuda and f.dtype == torch.int32 and f.device == device and f.is_contiguous():
+        # the steady-state case (a device int32 index tensor reused every step): no conversion calls
+        key = (f.data_ptr(), f._version, f.shape[0], bound, f.device)
+        if f.numel() and _faces_checked.get(key) is None:
+            lo, hi = int(f.min()), int(f.max())
+            if lo < 0 or hi >= bound:
+                raise IndexError("%s index out of range [0, %d): min %d max %d" % (what, bound, lo, hi))
+            _faces_checked.put(key, f)
+        return f
     if not f.is_cuda:
         if f.numel():
             lo, hi = int(f.min()), int(f.max())
@@ -248,7 +257,7 @@ class _Cfg:
                  "tex_hw", "vt_shared", "Vt", "B", "tex_view", "want_fim")
 
 
-def _args(cfg, vertices, faces, vt, ft, tex, fim):
+def _args(cfg, vertices, faces, vt, ft, tex, fim, vt_bstride):
     """NrRasterArgs of one call: sizes, flags and the caller's tensors (the library's own buffers are
     set from the arena layout, _Layout.fill)."""
     a = _lib.NrRasterArgs()
@@ -268,7 +277,7 @@ def _args(cfg, vertices, faces, vt, ft, tex, fim):
     a.face_index = fim.data_ptr()
     if cfg.flags & _lib.NR_DRAW_RGB:
         a.vertices_textures = vt.data_ptr()
-        a.vt_batch_stride = vt.stride(0)
+        a.vt_batch_stride = vt_bstride
         a.num_vertices_textures = cfg.Vt
         a.faces_textures = ft.data_ptr()
         tv = cfg.tex_view  # (data_ptr offset in elements, strides) of the [B, 3, H, W] view read
@@ -314,7 +323,7 @@ class _Layout:
     them needs a tensor of its own: one caching-allocator call per forward instead of up to eight.
     Computed once per configuration (sizes only) and cached."""
     __slots__ = ("nbytes", "frec", "fuv", "ws", "ws_bytes", "halo", "halo_bytes", "tex4", "bws", "bws_bytes",
-                 "fnorm", "vnorm")
+                 "fnorm", "vnorm", "bwd_need")
 
     def __init__(self, L, cfg, uv_items, want_halo, want_bws, tex_grad, nl):
         off = 0
@@ -342,12 +351,12 @@ class _Layout:
             if n <= _TEX_PACK_MAX_BYTES:  # per-item atlases of hundreds of MB are sampled in place
                 self.tex4 = take(n)
         self.bws = self.bws_bytes = None
-        if want_bws:
-            H, W = cfg.tex_hw
-            tex_items = (1 if cfg.tex_shared else B) if (rgb and tex_grad) else 0
-            n = L.nr_backward_workspace_bytes(B, F, V, tex_items, H, W, nl)
-            if n <= _BWD_PREZERO_MAX:
-                self.bws, self.bws_bytes = take(n), n
+        H, W = cfg.tex_hw
+        tex_items = (1 if cfg.tex_shared else B) if (rgb and tex_grad) else 0
+        # the backward's workspace for this configuration (its texture gradient follows tex_grad)
+        self.bwd_need = L.nr_backward_workspace_bytes(B, F, V, tex_items, H, W, nl)
+        if want_bws and self.bwd_need <= _BWD_PREZERO_MAX:
+            self.bws, self.bws_bytes = take(self.bwd_need), self.bwd_need
         self.fnorm = self.vnorm = None
         if nl:
             self.fnorm, self.vnorm = take(B * F * 3 * 4), take(B * V * 4 * 4)
@@ -391,8 +400,9 @@ class Rasterize(torch.autograd.Function):
     def forward(ctx, vertices, textures, vertices_textures, faces, faces_textures, backgrounds, light_recs, cfg):
         dev = vertices.device
         ctx.vt_shape = vertices_textures.shape
-        if vertices_textures.ndim == 3 and vertices_textures.shape[0] == 1 and cfg.B > 1:
-            vertices_textures = vertices_textures.expand(cfg.B, -1, -1)  # shared: batch stride 0
+        # a [1, Vt, 2] vt is shared by the batch: item stride 0 (NrRasterArgs.vt_batch_stride)
+        vt_shared = vertices_textures.ndim == 3 and (vertices_textures.shape[0] == 1 or vertices_textures.stride(0) == 0)
+        vt_bstride = 0 if vt_shared else (vertices_textures.stride(0) if vertices_textures.ndim == 3 else 0)
         B = cfg.B
         S = cfg.image_size * (2 if cfg.aa else 1)
         L = _lib.lib()
@@ -409,14 +419,14 @@ class Rasterize(torch.autograd.Function):
             return torch.empty((0, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev), fim
         rgb = bool(cfg.flags & _lib.NR_DRAW_RGB)
         grads = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        uv_items = (1 if vertices_textures.stride(0) == 0 else B) if rgb else 0
+        uv_items = (1 if vt_bstride == 0 else B) if rgb else 0
         nl = light_recs.shape[0] if light_recs is not None else 0
         lay = _layout(L, cfg, uv_items, _HALO_CACHE and grads, _BWD_PREZERO and grads,
                       ctx.needs_input_grad[1], nl)
         arena = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
         fim = torch.empty((B, S, S), dtype=torch.int32, device=dev)
         images = torch.empty((B, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev)
-        a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, fim)
+        a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, fim, vt_bstride)
         lay.fill(a, arena.data_ptr())
         if _FIM_FILL is not None:
             fim.fill_(_FIM_FILL)
@@ -481,9 +491,8 @@ class Rasterize(torch.autograd.Function):
         if want_tex:
             tex_items = 1 if cfg.tex_shared else cfg.B
             gt = torch.empty((tex_items, 3, H, W), dtype=torch.float32, device=dev)
-        nl = ctx.light[0].shape[0] if ctx.light is not None else 0
-        need = L.nr_backward_workspace_bytes(cfg.B, cfg.F, cfg.V, tex_items, H, W, nl)
         lay = ctx.layout
+        need = lay.bwd_need
         prezeroed = ctx.prezeroed and lay.bws_bytes == need
         ctx.prezeroed = False
         if prezeroed:
@@ -562,7 +571,7 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
         raise Exception  # rasterize.py:309-310
     _lib.require_gpu(vertices)
     dev = vertices.device
-    v = vertices.float().contiguous()
+    v = vertices if (vertices.dtype == torch.float32 and vertices.is_contiguous()) else vertices.float().contiguous()
     cfg = _Cfg()
     cfg.B, cfg.V = v.shape[0], v.shape[1]
     cfg.F = faces_t.shape[0]
@@ -571,7 +580,8 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
     cfg.backside = bool(hyperparams.draw_backside)
     cfg.flags = flags
     cfg.near, cfg.far, cfg.eps = float(hyperparams.near), float(hyperparams.far), float(hyperparams.eps)
-    cfg.C = _lib.lib().nr_num_channels(flags)
+    cfg.C = (3 if flags & _lib.NR_DRAW_RGB else 0) + (1 if flags & _lib.NR_DRAW_SILHOUETTES else 0) + \
+        (1 if flags & _lib.NR_DRAW_DEPTH else 0)  # nr_num_channels
     cfg.want_fim = bool(return_face_index)
     fi = _faces_i32(faces_t, dev, cfg.V, "faces")
     tex = vt = ft = None
@@ -583,7 +593,8 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
         vt = params.vertices_textures
         tex = params.textures
         _lib.require_gpu(vt, tex)
-        vt = vt.float()
+        if vt.dtype != torch.float32:
+            vt = vt.float()
         if vt.shape[0] not in (1, cfg.B):
             raise AssertionError("vertices_textures batch must be 1 or %d" % cfg.B)
         # the Function gets the [1, Vt, 2] source of a batch-shared vt (a slice of the expanded view,
@@ -597,7 +608,8 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
         ft = _faces_i32(params.faces_textures, dev, cfg.Vt, "faces_textures")
         if ft.shape[0] != cfg.F:
             raise AssertionError("faces_textures must have one row per face")
-        tex = tex.float()
+        if tex.dtype != torch.float32:
+            tex = tex.float()
         if tex.shape[0] not in (1, cfg.B):
             raise AssertionError("textures batch must be 1 or %d" % cfg.B)
         H, W = tex.shape[2], tex.shape[3]
@@ -619,7 +631,10 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
                 base = tex._base if tex._is_view() else None
                 tex = (base.reshape(1, 3, H, W) if base is not None and base.numel() == 3 * H * W
                        else torch.zeros((1, 3, H, W), dtype=torch.float32, device=dev))
-            item = tex[0]
+            # item 0 of the view: [3, H, W] at the view's own data pointer, contiguous when its strides
+            # are (H W, W, 1) (size-1 dimensions excepted) -- tested on the strides, without the view
+            st = tex.stride()
+            item_contig = st[1] == H * W and (H == 1 or st[2] == W) and (W == 1 or st[3] == 1)
             # the view's base takes the gradient in place of the view only when the gradient reaches
             # the caller's leaf through it: the view is not itself a leaf that requires grad
             # (that case was made per-item above), so its grad_fn, if any, is expand's of `base`
@@ -627,12 +642,12 @@ def rasterize_core(vertices, faces, params: RasterizeParam, hyperparams: Rasteri
             if base is not None and tex.requires_grad and not base.requires_grad:
                 base = None
             if (base is not None and base.numel() == 3 * H * W and base.is_contiguous()
-                    and item.is_contiguous() and item.data_ptr() == base.data_ptr()):
+                    and item_contig and tex.data_ptr() == base.data_ptr()):
                 tex = base
-            elif not item.is_contiguous():
-                tex = item.contiguous()[None]
+            elif not item_contig:
+                tex = tex[0].contiguous()[None]
             elif tex.shape[0] != 1:
-                tex = item[None]
+                tex = tex[0][None]
             cfg.tex_view = (0, 0, H * W, 1)
         else:
             cfg.tex_view = (0, tex.stride(0), tex.stride(1), tex.stride(3))

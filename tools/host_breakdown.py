@@ -126,5 +126,25 @@ def main():
         print("%-32s host %8.1f us/call   with GPU %8.1f us/call" % (name, h, a), flush=True)
 
 
+
+    # the autograd engine hands a CUDA backward to its device thread and waits for it; with
+    # multithreading off it runs the backward in the calling thread (a user-side setting)
+    torch.autograd.set_multithreading_enabled(False)
+    h, a = per_call_us(step)
+    print("%-32s host %8.1f us/call   with GPU %8.1f us/call" % ("step (autograd single-thread)", h, a), flush=True)
+    h, a = per_call_us(tiny_autograd)
+    print("%-32s host %8.1f us/call   with GPU %8.1f us/call" % ("tiny autograd (single-thread)", h, a), flush=True)
+    import cProfile
+    import pstats
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(N):
+        step()
+    pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    torch.autograd.set_multithreading_enabled(True)
+
+
 if __name__ == "__main__":
     main()

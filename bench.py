@@ -439,6 +439,22 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         gather_ms = float(t.item())
 
+    # the host's enqueue time per step with the autograd engine running the backward in the calling
+    # thread (torch.autograd.set_multithreading_enabled(False), a user-side setting): by default the
+    # engine hands a CUDA backward to its device thread and waits, which costs 50-110 us of host time
+    # per step on these boxes (tools/host_breakdown.py).  Reported beside host_ms_per_step; the timed
+    # steps above run with torch's defaults.
+    torch.cuda.synchronize()
+    with torch.autograd.set_multithreading_enabled(False):
+        for _ in range(2):
+            step(w)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step(w)
+        host_single = (time.perf_counter() - t1) / args.steps * 1e3
+        torch.cuda.synchronize()
+
     graph_ms = None
     if args.graph_steps > 0:
         images = images.detach()  # release the last eager step's autograd graph before the capture
@@ -521,6 +537,7 @@ def main():
                    "global_batch": world * args.batch, "image_size": args.image_size, "faces": w["F"],
                    "channels": w["C"], "parallelism": "batch-sharded dp%d" % world},
         "host_ms_per_step": round(host_elapsed / args.steps * 1e3, 4),
+        "host_ms_per_step_autograd_single_thread": round(host_single, 4),
         "roofline": {"bound": bound, "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(hbm_frac, 5), "traffic": traffic,
                      "traffic_source": pmc_note, "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5),

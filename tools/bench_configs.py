@@ -107,8 +107,13 @@ def cfg2(dev, a):
                                    textures=tex[None].expand(B, -1, -1, -1))
         nr.rasterize_core(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
     t = median_step(step, a.steps, a.warmup)
+    # the same eager step with the autograd engine in the calling thread (a user-side setting that
+    # removes the engine's hand-over to its device thread; see bench.py)
+    with torch.autograd.set_multithreading_enabled(False):
+        t1 = median_step(step, a.steps, a.warmup)
     res = dict(config="cfg2 teapot B=4 256^2 rgb+sil+depth", faces=int(f.shape[0]), batch=B, image_size=s,
                ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
+               eager_single_thread_autograd_ms_per_step=round(t1 * 1e3, 4),
                kernels_ms=kernels_ms(step))
     proj.grad = tex.grad = None
     tg = median_step(graphed(step), a.steps, a.warmup)

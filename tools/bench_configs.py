@@ -6,8 +6,10 @@
   cfg5  example2-style loop: torus 250x100 (50000 faces) at 512^2 (1024^2 internal), silhouettes,
         200 fwd+bwd steps with an Adam update of the vertices
 
-One step = rasterize_core forward + backward (cfg5: plus the Adam step), inputs resident on the GPU,
-median of the per-step times over --steps steps after --warmup.  Prints one JSON line per config.
+One step = rasterize_core forward + backward (cfg5: plus the Adam step), inputs resident on the GPU.
+ms_per_step times --steps steps between two synchronisations after --warmup (bench.py's method: the
+host enqueues a step while the GPU runs the previous one); synced_ms_per_step is the median with a
+synchronisation after every step (host and GPU time in series).  Prints one JSON line per config.
 cfg2 is also timed as a HIP-graph replay of the captured step (graph_ms_per_step): at B=4 the eager
 step is bound by host launch overhead, not by the kernels.
 cfg1 is the reference's CPU-only plumbing case and cfg4 is bench.py --gpus 8.
@@ -35,6 +37,8 @@ subdivide = synthetic.subdivide  # (moved to the package: tests use it too)
 
 
 def median_step(fn, steps, warmup):
+    """Median of per-step times with a synchronisation after every step (a step's host enqueue and
+    its GPU work in series)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -45,6 +49,19 @@ def median_step(fn, steps, warmup):
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     return float(np.median(ts))
+
+
+def pipelined_step(fn, steps, warmup):
+    """bench.py's timing: `steps` steps bracketed by synchronisations, so the host enqueues a step
+    while the GPU runs the previous one (what a training loop without a per-step sync sees)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
 
 
 def kernels_ms(fn, n=5):
@@ -106,14 +123,18 @@ def cfg2(dev, a):
         params = nr.RasterizeParam(vertices_textures=vt_d[None].expand(B, -1, -1), faces_textures=ft_d,
                                    textures=tex[None].expand(B, -1, -1, -1))
         nr.rasterize_core(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
-    t = median_step(step, a.steps, a.warmup)
-    # the same eager step with the autograd engine in the calling thread (a user-side setting that
+    t = pipelined_step(step, a.steps, a.warmup)
+    ts = median_step(step, a.steps, a.warmup)
+    # the same eager steps with the autograd engine in the calling thread (a user-side setting that
     # removes the engine's hand-over to its device thread; see bench.py)
     with torch.autograd.set_multithreading_enabled(False):
-        t1 = median_step(step, a.steps, a.warmup)
+        t1 = pipelined_step(step, a.steps, a.warmup)
+        t1s = median_step(step, a.steps, a.warmup)
     res = dict(config="cfg2 teapot B=4 256^2 rgb+sil+depth", faces=int(f.shape[0]), batch=B, image_size=s,
                ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
-               eager_single_thread_autograd_ms_per_step=round(t1 * 1e3, 4),
+               synced_ms_per_step=round(ts * 1e3, 4),
+               single_thread_autograd_ms_per_step=round(t1 * 1e3, 4),
+               single_thread_autograd_synced_ms_per_step=round(t1s * 1e3, 4),
                kernels_ms=kernels_ms(step))
     proj.grad = tex.grad = None
     tg = median_step(graphed(step), a.steps, a.warmup)
@@ -145,10 +166,11 @@ def cfg3_step(dev):
 
 def cfg3(dev, a):
     step, f, B, s = cfg3_step(dev)
-    t = median_step(step, a.steps, a.warmup)
+    t = pipelined_step(step, a.steps, a.warmup)
+    ts = median_step(step, a.steps, a.warmup)
     return dict(config="cfg3 car (1x subdivided) B=64 256^2 textured rgba", faces=int(f.shape[0]), batch=B,
                 image_size=s, ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
-                kernels_ms=kernels_ms(step))
+                synced_ms_per_step=round(ts * 1e3, 4), kernels_ms=kernels_ms(step))
 
 
 def cfg5(dev, a):
@@ -168,7 +190,8 @@ def cfg5(dev, a):
         loss = ((ren.render_silhouettes(verts, faces) - target) ** 2).sum()
         loss.backward()
         opt.step()
-    t = median_step(step, a.steps, a.warmup)
+    t = pipelined_step(step, a.steps, a.warmup)
+    ts = median_step(step, a.steps, a.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.loop_steps):
@@ -177,7 +200,8 @@ def cfg5(dev, a):
     loop = time.perf_counter() - t0
     res = dict(config="cfg5 torus 50k faces, 512^2 (1024^2 internal) silhouettes, Renderer + Adam loop",
                faces=int(f.shape[0]), batch=1, image_size=s, ms_per_step=round(t * 1e3, 4),
-               mpx_per_s=round(s * s / t / 1e6, 1), loop_steps=a.loop_steps, loop_s=round(loop, 4),
+               mpx_per_s=round(s * s / t / 1e6, 1), synced_ms_per_step=round(ts * 1e3, 4),
+               loop_steps=a.loop_steps, loop_s=round(loop, 4),
                kernels_ms=kernels_ms(step))
     # the same loop as one captured HIP graph per step: device-resident viewpoint, capturable Adam
     ren.viewpoints = torch.as_tensor(ren.viewpoints, dtype=torch.float32, device=dev)

@@ -346,7 +346,9 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     hipStream_t st = (hipStream_t)stream;
     const int S = a->anti_aliasing ? 2 * a->image_size : a->image_size;
     Geom g = make_geom(a->num_faces, S);
-    g.group = group_for(a->batch_size, rgb && !a->tex_stride_b ? BWD_GROUP_TEX : BWD_GROUP);
+    const bool hot_texels = rgb && !a->tex_stride_b &&
+                            (long long)a->tex_height * a->tex_width > BWD_HOT_TEXELS_PER_FACE * a->num_faces;
+    g.group = group_for(a->batch_size, hot_texels ? BWD_GROUP_TEX : BWD_GROUP);
     const int HW = a->tex_height * a->tex_width;
     const int HWp = (HW + 3) & ~3;
     char* w = (char*)workspace;

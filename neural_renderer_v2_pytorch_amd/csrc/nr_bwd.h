@@ -56,16 +56,29 @@ static_assert(BWD_LDS_IG % 16 == 0, "halo staging alignment");
 // per-wave phase timestamps (timing builds only, tools/bwd_timing.py): lane 0 of every wave of the
 // 2-pixel variant records the shader clock at 8 points of its life
 #ifdef NR_BWD_TIMING
-constexpr long long NR_TIMING_MAX = 1 << 22;
+constexpr long long NR_TIMING_MAX = 1 << 23;
+constexpr int NR_BSLOTS = 10;  // per wave: 8 phase slots, then the wall clock (100 MHz, chip-wide) at entry and exit
 __device__ unsigned long long g_bwd_t[NR_TIMING_MAX];
 #define NR_TSTAMP(k)                                                                                       \
     do {                                                                                                   \
-        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 8 + (k); \
+        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * NR_BSLOTS + (k); \
         const unsigned long long t_ = clock64();                                                           \
         if ((threadIdx.x & 63) == 0 && i_ < NR_TIMING_MAX) g_bwd_t[i_] = t_;                                 \
     } while (0)
 #else
 #define NR_TSTAMP(k) \
+    do {             \
+    } while (0)
+#endif
+#ifdef NR_BWD_TIMING
+#define NR_WSTAMP(k)                                                                                         \
+    do {                                                                                                     \
+        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * NR_BSLOTS + (k); \
+        const unsigned long long t_ = wall_clock64();                                                      \
+        if ((threadIdx.x & 63) == 0 && i_ < NR_TIMING_MAX) g_bwd_t[i_] = t_;                                 \
+    } while (0)
+#else
+#define NR_WSTAMP(k) \
     do {             \
     } while (0)
 #endif
@@ -226,7 +239,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     // a tile with no foreground pixel contributes nothing (every gradient term is per foreground
     // pixel; the halo only feeds foreground pixels' stencils): with the forward's bin flags it ends
     // here.  Backgrounds (BG) get gradient from background pixels, so that instantiation never skips.
-    if (!BG && a.binfg && a.binfg[(long long)b * g.nbins + (ty0 / COARSE) * g.nbx + tx0 / COARSE] == 0) return;
+    NR_WSTAMP(8);
+    if (!BG && a.binfg && a.binfg[(long long)b * g.nbins + (ty0 / COARSE) * g.nbx + tx0 / COARSE] == 0) {
+        NR_WSTAMP(9);
+        return;
+    }
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     const int bt = sh.tv.sb ? b : 0;
@@ -798,9 +815,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         }
     }
     NR_TSTAMP(6);
+    NR_WSTAMP(9);
 #ifdef NR_BWD_TIMING
     {
-        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 8 + 7;
+        const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * NR_BSLOTS + 7;
         if (lane == 0 && i_ < NR_TIMING_MAX) g_bwd_t[i_] = (unsigned long long)nfaces_dbg;
     }
 #endif

@@ -225,6 +225,7 @@ __device__ __forceinline__ int count_bucket(int c) { return c <= 0 ? 0 : min(ORD
 // the chunk's lanes of the same bucket.  Stable: screen order (and so neighbouring bins, which share
 // face records in L2) within a bucket -- an unstable order cost the car's forward ~6 us.
 constexpr int ORDER_MAX_ENTRIES = 64 * 256;
+// (ORDER_EMPTY, the entry flag of a bin without candidates, is in nr_common.h with ordered_bin)
 __global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt, int* __restrict__ order, int B,
                                                     int nbins) {
     __shared__ int s_h[ORDER_MAX_ENTRIES / 64][ORDER_BUCKETS];
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt,
             const unsigned long long m = __ballot(bk == b);
             if (bk == b) rank = __popcll(m & lt);
         }
-        if (k < n) out[s_h[ch][bk] + rank] = e;
+        if (k < n) out[s_h[ch][bk] + rank] = e | (bk == 0 ? ORDER_EMPTY : 0);
     }
 }
 
@@ -535,7 +536,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 
     const int S = g.S;
     int b, bin_x, bin_y;
-    if (order) ordered_bin(order, gridDim.y, g.nbins, g.nbx, b, bin_x, bin_y);
+    bool known_empty = false;  // (ordered) the setup's counts say the bin has no candidate face
+    if (order) known_empty = ordered_bin(order, gridDim.y, g.nbins, g.nbx, b, bin_x, bin_y);
     else block_item_tile(g.group, g.nbx, g.nby, b, bin_x, bin_y);
     const int bin = bin_y * g.nbx + bin_x;
     const int bx0 = bin_x * COARSE;
@@ -553,16 +555,17 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     unsigned long long t_stage = 0;
 #endif
     // the first round of mask words and its candidate count
-    const uint32_t bits0 = (t < g.nwords) ? words[t] : 0u;
-    int total0;
-    const int off0 = block_scan<C::NW>(__builtin_popcount(bits0), total0, s_scan);
+    const uint32_t bits0 = (!known_empty && t < g.nwords) ? words[t] : 0u;
+    int total0 = 0;
+    const int off0 = known_empty ? 0 : block_scan<C::NW>(__builtin_popcount(bits0), total0, s_scan);
     NR_FTSTAMP(1, clock64());
     // one staging round holds every candidate of the bin (the usual case): the waves take the 16 8x8
     // blocks one at a time from a counter, so a wave that meets few faces goes on to another block
     // instead of idling at the block's end (static quadrants keep 80 % of the waves' time busy on the
     // headline, dealt blocks ~92 %, CPU-counted; measured fwd 0.212 -> 0.208 ms)
     // (not with 16 waves: one block each already; measured 0.824 -> 0.918 ms on the car)
-    const bool dyn = NTF < 1024 && g.nwords <= NTF && total0 <= FCAP;
+    // (a known-empty bin takes this path too: it only writes its empty outputs)
+    const bool dyn = known_empty || (NTF < 1024 && g.nwords <= NTF && total0 <= FCAP);
     int ncand = 0;  // the bin's candidate faces (block-uniform)
     unsigned short* s_slot = reinterpret_cast<unsigned short*>(s_cand);  // (dyn, SHADE) winners' staging slots
     static_assert(!SHADE || CAND * 4 >= COARSE * COARSE * 2, "slot map in the candidate list's space");

@@ -48,10 +48,10 @@ from neural_renderer_v2_pytorch_amd import _lib  # noqa: E402
 L = _lib.lib()
 S = 2 * size
 blocks = (S // 32) * (S // 16) * batch
-n = blocks * 4 * 8
+n = blocks * 4 * 10
 buf = (ctypes.c_ulonglong * n)()
 assert L.nr_debug_bwd_timing(buf, ctypes.c_size_t(n)) == 0
-t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(blocks, 4, 8)
+t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(blocks, 4, 10)
 names = ["step1", "barrier1", "stencil", "barrier2", "stage+group", "gather+atomics"]
 d = np.diff(t[:, :, :7], axis=2)
 life = t[:, :, 6] - t[:, :, 0]
@@ -80,3 +80,14 @@ held = (bend - start).sum()
 idle = (bend - end).sum()
 print("foreground blocks %d: slot time idle after a wave's end %.3f of the time the block holds its slots"
       % (fg.sum(), idle / held))
+
+# timeline from the chip-wide wall clock (100 MHz), per block: when the foreground (not skipped) and the
+# skipped tiles start and end relative to the kernel's first wave
+ws_, we_ = t[:, :, 8].min(axis=1), t[:, :, 9].max(axis=1)
+t0 = ws_.min()
+print("kernel span %.1f us (wall clock)" % ((we_.max() - t0) / 100.0))
+for lab, sel in (("skipped tiles", ~fg), ("foreground tiles", fg)):
+    if sel.any():
+        st_, en_ = (ws_[sel] - t0) / 100.0, (we_[sel] - t0) / 100.0
+        print("   %-17s %6d blocks  start mean %7.1f max %7.1f us   end mean %7.1f max %7.1f us   duration mean %6.1f max %6.1f us" % (
+            lab, sel.sum(), st_.mean(), st_.max(), en_.mean(), en_.max(), (en_ - st_).mean(), (en_ - st_).max()))

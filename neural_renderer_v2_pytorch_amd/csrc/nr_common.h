@@ -208,6 +208,19 @@ __device__ __forceinline__ unsigned long long lane_mask_ule(float a, float b) { 
 __device__ __forceinline__ float lane_value(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+// the maximum of v over the wave's 64 lanes (all active), wave-uniform; NaN lanes are ignored unless
+// every lane is NaN.  A row_shr max chain leaves each 16-lane row's maximum in its lane 15 (a lane
+// whose DPP source is outside its row keeps its own value).
+__device__ __forceinline__ float wave_max(float v) {
+    float r = v;
+#define NR_MAX_SHR(ctrl) r = fmaxf(r, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(r), __float_as_int(r), ctrl, 0xf, 0xf, false)))
+    NR_MAX_SHR(0x111);  // row_shr:1
+    NR_MAX_SHR(0x112);  // row_shr:2
+    NR_MAX_SHR(0x114);  // row_shr:4
+    NR_MAX_SHR(0x118);  // row_shr:8
+#undef NR_MAX_SHR
+    return fmaxf(fmaxf(lane_value(r, 15), lane_value(r, 31)), fmaxf(lane_value(r, 47), lane_value(r, 63)));
+}
 
 // |x| in [2^-e, 2^e]
 __device__ __forceinline__ bool in_range(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }

@@ -330,6 +330,36 @@ def test_face_index_dense_snapped_soup(oracle_mod, dev, S, F, seed):
     assert np.array_equal(fim2.cpu().numpy(), ref), int((fim2.cpu().numpy() != ref).sum())
 
 
+@pytest.mark.parametrize("zlevels", [0, 3])
+def test_face_index_deep_stack_depth_cull(oracle_mod, dev, zlevels):
+    """Bins of 1000+ small faces at random depths (zlevels > 0: only that many distinct depths, so
+    many faces tie within depth_min_delta): the deep variant's deep-first order, its empty-bin skip and
+    its wave-level depth cull (k_raster_fwd walk_block<..., ZCULL>, bins of >= 512 candidates) drop
+    faces behind every pixel of a wave in the ballot; bit-exact against the brute-force oracle."""
+    r = np.random.RandomState(7 + zlevels)
+    S, F, B = 64, 4000, 2
+    cx = r.uniform(-0.9, 0.9, size=(B, F, 1))
+    cy = r.uniform(-0.9, 0.9, size=(B, F, 1))
+    x = (cx + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    y = (cy + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    if zlevels:
+        z = np.repeat(r.choice(np.linspace(1.0, 3.0, zlevels), size=(B, F, 1)), 3, axis=2).astype(np.float32)
+    else:
+        z = r.uniform(0.5, 5.0, size=(B, F, 3)).astype(np.float32)
+    x[1] = np.abs(cx[1]) + 0.15 + (x[1] - cx[1])  # item 1: nothing in its left bins (empty, flagged)
+    fg = np.stack([x, y, z], -1).astype(np.float32)
+    ref = oracle_mod.face_index_map(torch.as_tensor(fg), S)
+    verts = torch.as_tensor(fg.reshape(B, F * 3, 3), device=dev)
+    faces = torch.arange(F * 3, dtype=torch.int32, device=dev).reshape(F, 3)
+    hp = nr.RasterizeHyperparam(image_size=S, anti_aliasing=False)
+    hp.draw_rgb = False
+    _, fim = nrr.rasterize_core(verts, faces, nr.RasterizeParam(), hp, return_face_index=True)
+    ntf, flags = _lib.last_launch("k_raster_fwd")
+    assert ntf == 1024 and flags & _lib.NR_LAUNCH_DEEP_FIRST, (ntf, flags)
+    assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
+    assert (ref[1] >= 0).any() and (ref[1] < 0).any()
+
+
 def test_headline_properties(dev):
     """Full headline config (B=64, 256^2 AA, ico 5120, rgb+sil+depth): size-independent properties."""
     B = 64

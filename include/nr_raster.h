@@ -262,7 +262,8 @@ NR_API int nr_profile_read(const char* kernel, float* ms);
  * 32x32 bin, 1024 = one wave per 8x8 block; k_raster_bwd: 256 = 2 pixels per lane, 512 = 1 pixel
  * per lane) and flags = NR_LAUNCH_* bits.  NR_ERR_ARGS when none was recorded. */
 enum { NR_LAUNCH_FUSED_SHADE = 1, NR_LAUNCH_STATIC_CHANNELS = 2, NR_LAUNCH_TWO_PX_PER_LANE = 4,
-       NR_LAUNCH_DEEP_FIRST = 8 /* k_raster_fwd: bins dispatched deepest first (k_bin_order) */ };
+       NR_LAUNCH_DEEP_FIRST = 8 /* k_raster_fwd: bins dispatched deepest first (k_bin_order) */,
+       NR_LAUNCH_SPLIT = 16 /* k_raster_fwd: deep bins at 1024 threads, the rest at 256 on a side stream */ };
 NR_API int nr_last_launch(const char* kernel, int* block_threads, int* flags);
 
 #ifdef __cplusplus

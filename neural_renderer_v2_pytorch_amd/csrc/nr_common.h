@@ -78,6 +78,7 @@ struct ProfScope {  // records the start/end events of one launch when profiling
 struct Geom {
     int S, nbx, nby, nbins, nwords, tiles_x, tiles_y;
     int group;  // item-interleave group of the raster launches (block_item_tile); 0: per-item bands
+    int B;      // items (the ordered forward's lists; set by run_face_index)
 };
 
 Geom make_geom(int F, int S) {
@@ -90,6 +91,7 @@ Geom make_geom(int F, int S) {
     g.tiles_x = (S + TW - 1) / TW;
     g.tiles_y = (S + TH - 1) / TH;
     g.group = 0;
+    g.B = 0;
     return g;
 }
 
@@ -99,7 +101,7 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // [bin order i32 B*nbins] (the last two: deep-bin dispatch order, run_face_index)
 size_t ws_bbox_bytes(int B, int F) { return align_up((size_t)B * F * sizeof(int2)); }
 size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins * g.nwords * 4); }
-size_t ws_order_bytes(int B, const Geom& g) { return 2 * align_up((size_t)B * g.nbins * 4); }
+size_t ws_order_bytes(int B, const Geom& g) { return 2 * align_up((size_t)B * g.nbins * 4) + 256; }  // + the split counts
 
 // ------------------------------------------------------------------------------------------------
 // device helpers
@@ -654,19 +656,29 @@ __device__ __forceinline__ void block_item_tile(int G, int nx, int ny, int& b, i
 }
 // The (item, bin) of a forward block from the deep-first dispatch order (k_bin_order): with B a
 // multiple of 8, list x (items = x mod 8) is read by the blocks dealt to XCD x (L % 8 = x), so an
-// item's bins stay on one XCD as with block_item_tile; otherwise one list for the whole grid.  Returns
-// true when the entry carries ORDER_EMPTY (no candidate face: the block skips the bin-mask scan).
+// item's bins stay on one XCD as with block_item_tile; otherwise one list for the whole grid.  part:
+// 0 = the whole list, 1 = its deep prefix [0, split[x]), 2 = the rest (the split launches of
+// run_face_index).  Returns -1 past the block's part (the block ends), 1 when the entry carries
+// ORDER_EMPTY (no candidate face: the block skips the bin-mask scan), else 0.
 constexpr int ORDER_EMPTY = 1 << 30;
-__device__ __forceinline__ bool ordered_bin(const int* __restrict__ order, int B, int nbins, int nbx, int& b,
-                                            int& tx, int& ty) {
+__device__ __forceinline__ int ordered_bin(const int* __restrict__ order, const int* __restrict__ split, int part, int B,
+                                           int nbins, int nbx, int& b, int& tx, int& ty) {
     const int L = blockIdx.y * gridDim.x + blockIdx.x;
-    const int oe = (B % 8 == 0) ? order[(L & 7) * ((B >> 3) * nbins) + (L >> 3)] : order[L];
+    const bool per_xcd = B % 8 == 0;
+    const int x = per_xcd ? (L & 7) : 0;
+    const int n = per_xcd ? (B >> 3) * nbins : B * nbins;
+    int r = per_xcd ? (L >> 3) : L;
+    int hi = n;
+    if (part == 1) hi = split[x];
+    else if (part == 2) r += split[x];
+    if (r >= hi) return -1;
+    const int oe = order[x * n + r];
     const int e = oe & (ORDER_EMPTY - 1);
     b = e / nbins;
     const int bin = e - b * nbins;
     ty = bin / nbx;
     tx = bin - ty * nbx;
-    return (oe & ORDER_EMPTY) != 0;
+    return (oe & ORDER_EMPTY) ? 1 : 0;
 }
 // the interleave group for B items and a preferred group size: the preference when it divides B, else
 // all B items; 0 (per-item bands) when B is not a multiple of 8

@@ -226,8 +226,10 @@ __device__ __forceinline__ int count_bucket(int c) { return c <= 0 ? 0 : min(ORD
 // face records in L2) within a bucket -- an unstable order cost the car's forward ~6 us.
 constexpr int ORDER_MAX_ENTRIES = 64 * 256;
 // (ORDER_EMPTY, the entry flag of a bin without candidates, is in nr_common.h with ordered_bin)
+// split (optional): per list, the length of its prefix of bins with >= 2^(split_bucket - 1) candidate
+// faces, at most cap (the deep launch of a split forward, run_face_index)
 __global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt, int* __restrict__ order, int B,
-                                                    int nbins) {
+                                                    int nbins, int* __restrict__ split, int split_bucket, int cap) {
     __shared__ int s_h[ORDER_MAX_ENTRIES / 64][ORDER_BUCKETS];
     __shared__ int s_base[ORDER_BUCKETS];
     const bool per_xcd = gridDim.x == 8;
@@ -280,6 +282,11 @@ __global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt,
             if (bk == b) rank = __popcll(m & lt);
         }
         if (k < n) out[s_h[ch][bk] + rank] = e | (bk == 0 ? ORDER_EMPTY : 0);
+    }
+    if (split && threadIdx.x == 0) {  // (s_base still holds the bucket totals)
+        int d = 0;
+        for (int bb = split_bucket; bb < ORDER_BUCKETS; bb++) d += s_base[bb];
+        split[x] = min(d, cap);
     }
 }
 
@@ -533,7 +540,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                                                   int F, Geom g, float near, float far, float delta,
                                                   int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
                                                   float* __restrict__ halo, uint8_t* __restrict__ binfg,
-                                                  const int* __restrict__ order, int fim_sparse) {
+                                                  const int* __restrict__ order, int fim_sparse,
+                                                  const int* __restrict__ split, int part) {
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
@@ -547,8 +555,13 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     const int S = g.S;
     int b, bin_x, bin_y;
     bool known_empty = false;  // (ordered) the setup's counts say the bin has no candidate face
-    if (order) known_empty = ordered_bin(order, gridDim.y, g.nbins, g.nbx, b, bin_x, bin_y);
-    else block_item_tile(g.group, g.nbx, g.nby, b, bin_x, bin_y);
+    if (order) {
+        const int ob = ordered_bin(order, split, part, g.B, g.nbins, g.nbx, b, bin_x, bin_y);
+        if (ob < 0) return;  // past this launch's part of the list (block-uniform, before any barrier)
+        known_empty = ob == 1;
+    } else {
+        block_item_tile(g.group, g.nbx, g.nby, b, bin_x, bin_y);
+    }
     const int bin = bin_y * g.nbx + bin_x;
     const int bx0 = bin_x * COARSE;
     const int by0 = bin_y * COARSE;
@@ -566,8 +579,22 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 #endif
     // the first round of mask words and its candidate count
     const uint32_t bits0 = (!known_empty && t < g.nwords) ? words[t] : 0u;
-    int total0 = 0;
-    const int off0 = known_empty ? 0 : block_scan<C::NW>(__builtin_popcount(bits0), total0, s_scan);
+    // (256-thread variant, NTF < nwords <= 2 NTF, e.g. the car's shallow bins in a split forward) the
+    // second round of words too, scanned in the same block scan (two 16-bit counts per thread), so a
+    // bin whose candidates fit one staging round takes the dealt-block path
+    constexpr bool TWO = NTF < 1024;
+    const bool two = TWO && !known_empty && g.nwords > NTF && g.nwords <= 2 * NTF;
+    const uint32_t bits1 = (two && t + NTF < g.nwords) ? words[t + NTF] : 0u;
+    int total0 = 0, total1 = 0, off1 = 0;
+    int off0 = 0;
+    if (!known_empty) {
+        int tot;
+        const int off = block_scan<C::NW>(__builtin_popcount(bits0) | (__builtin_popcount(bits1) << 16), tot, s_scan);
+        off0 = off & 0xffff;
+        total0 = tot & 0xffff;
+        off1 = off >> 16;
+        total1 = tot >> 16;
+    }
     NR_FTSTAMP(1, clock64());
     // one staging round holds every candidate of the bin (the usual case): the waves take the 16 8x8
     // blocks one at a time from a counter, so a wave that meets few faces goes on to another block
@@ -575,12 +602,12 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     // headline, dealt blocks ~92 %, CPU-counted; measured fwd 0.212 -> 0.208 ms)
     // (not with 16 waves: one block each already; measured 0.824 -> 0.918 ms on the car)
     // (a known-empty bin takes this path too: it only writes its empty outputs)
-    const bool dyn = known_empty || (NTF < 1024 && g.nwords <= NTF && total0 <= FCAP);
+    const bool dyn = known_empty || (NTF < 1024 && (g.nwords <= NTF || two) && total0 + total1 <= FCAP);
     int ncand = 0;  // the bin's candidate faces (block-uniform)
     unsigned short* s_slot = reinterpret_cast<unsigned short*>(s_cand);  // (dyn, SHADE) winners' staging slots
     static_assert(!SHADE || CAND * 4 >= COARSE * COARSE * 2, "slot map in the candidate list's space");
     if (dyn) {
-        ncand = total0;
+        ncand = total0 + total1;
         if (ncand == 0) {
             for (int u = wid; u < 16 && !fim_sparse; u += C::NW) {
                 const int px = bx0 + (u & 3) * 8 + (lane & 7), py = by0 + (u >> 2) * 8 + (lane >> 3);
@@ -589,6 +616,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         } else {
             int r = off0;
             for (uint32_t m = bits0; m; m &= m - 1, r++) s_cand[r] = t * 32 + __builtin_ctz(m);
+            r = total0 + off1;
+            for (uint32_t m = bits1; m; m &= m - 1, r++) s_cand[r] = (t + NTF) * 32 + __builtin_ctz(m);
             if (t == 0) s_next = 0;
             __syncthreads();
 #ifdef NR_FWD_TIMING

@@ -80,12 +80,41 @@ size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
     return ws_bbox_bytes(batch_size, num_faces) + ws_mask_bytes(batch_size, g) + ws_order_bytes(batch_size, g);
 }
 
+// A side stream per (host thread, device) for the split forward, with its fork / join events; created
+// on first use outside a stream capture (null: no split for this call)
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+#ifndef NR_SPLIT_BUCKET
+#define NR_SPLIT_BUCKET 10
+#endif
+constexpr int SPLIT_BUCKET = NR_SPLIT_BUCKET;  // deep bins: >= 512 candidates
+SideStream* side_stream(hipStream_t st) {
+    static thread_local SideStream tab[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream& x = tab[dev];
+    if (!x.s) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+        if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess ||
+            hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) {
+            x.s = nullptr;
+            return nullptr;
+        }
+    }
+    return &x;
+}
+
 static int run_face_index(const float* vertices, const int32_t* faces_idx, float* face_records, int32_t* fim,
                           int B, int V, int F, int S, float near, float far, int draw_backside, float delta,
                           void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images,
                           TexPack pk, ZeroFill zf = ZeroFill{nullptr, 0}) {
     Geom g = make_geom(F, S);
     g.group = group_for(B, FWD_GROUP);
+    g.B = B;
     int2* bbox = (int2*)ws;
     uint32_t* mask = (uint32_t*)((char*)ws + ws_bbox_bytes(B, F));
     int* bin_count = (int*)((char*)mask + ws_mask_bytes(B, g));
@@ -144,17 +173,29 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             if (e) return e;
         }
     }
-    if (ordered) {
-        hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_count, bin_order, B, g.nbins);
-        const int e = check_launch("k_bin_order");
-        if (e) return e;
-    }
-    const int* order = ordered ? bin_order : nullptr;
     // k_shade's work fused into the forward's 256-thread variant (anti-aliasing, no lights or
     // backgrounds): the face-index map is not read back, and there is one launch fewer
     const Shade sh = ra ? make_shade(ra) : Shade{};
     // the deep-bin / small-grid 1024-thread variant shades too (its threads 0-255)
     const bool fuse = ra && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
+    // split forward (deep-bin batches of B % 8 == 0 items, e.g. the car): the bins with >= 2^(SPLIT_BUCKET
+    // - 1) candidates (a prefix of each deep-first list, at most Bcap / 8 * nbins of them) in the
+    // 1024-thread variant on the caller's stream, the rest in the 256-thread variant on a side stream at
+    // the same time: a shallow bin's 16 waves in the 1024-thread variant mostly wait for their block's
+    // slowest wave, where the 256-thread variant deals its 16 8x8 blocks to 4 waves
+    const int Bcap = B % 8 == 0 ? max(8, (B / 4 + 7) / 8 * 8) : 0;
+    int* split_cnt = (int*)((char*)bin_order + align_up((size_t)B * g.nbins * 4));
+    SideStream* side = nullptr;
+#ifndef NR_NO_SPLIT
+    if (ordered && fuse && B % 8 == 0 && Bcap <= B) side = side_stream(st);
+#endif
+    if (ordered) {
+        hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_count, bin_order, B, g.nbins,
+                           side ? split_cnt : nullptr, SPLIT_BUCKET, Bcap / 8 * g.nbins);
+        const int e = check_launch("k_bin_order");
+        if (e) return e;
+    }
+    const int* order = ordered ? bin_order : nullptr;
     // per-bin foreground flags after the halo values (the backward skips background tiles)
     uint8_t* binfg = (ra && ra->halo) ? (uint8_t*)ra->halo + halo_flags_offset_bytes(B, S, sh.C) : nullptr;
     // empty bins leave their -1 face ids unwritten (NrRasterArgs.face_index_sparse): with the fused
@@ -165,22 +206,42 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         const int rs = vertices ? FACE_REC : 9;
         g_last_fwd = LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
                                (fuse && ntf == 256 && sh.C == MAXC ? NR_LAUNCH_STATIC_CHANNELS : 0) |
-                               (ordered ? NR_LAUNCH_DEEP_FIRST : 0)};
-        if (fuse && ntf == 1024)
+                               (ordered ? NR_LAUNCH_DEEP_FIRST : 0) | (side ? NR_LAUNCH_SPLIT : 0)};
+        if (side) {
+            // fork: the side stream waits for the setup and the order; join: the caller's stream waits
+            // for the side stream's launch
+            if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+                return check_launch("hipEventRecord");
+            hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, Bcap), dim3(1024), 0, st, face_records, rs, bbox,
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 1);
+            int e = check_launch("k_raster_fwd");
+            if (e) return e;
+            if (sh.C == MAXC)
+                hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
+                                   bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
+                                   split_cnt, 2);
+            else
+                hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs, bbox,
+                                   mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 2);
+            e = check_launch("k_raster_fwd");
+            if (e) return e;
+            if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess)
+                return check_launch("hipEventRecord");
+        } else if (fuse && ntf == 1024)
             hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
             hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse)
             hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse);
+                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (ntf == 256)
             hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0);
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
         else
             hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0);
+                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra || fuse) return e;

@@ -135,7 +135,7 @@ def test_cfg3_car_subdivided_vs_oracle(oracle_mod, dev):
     pv = proj.to(dev).requires_grad_(True)
     img, fim = nrr.rasterize_core(pv, torch.as_tensor(f, device=dev), params, hp, return_face_index=True)
     assert img.shape == (B, 4, s, s)
-    assert _lib.last_launch("k_raster_fwd") == (1024, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_DEEP_FIRST)
+    assert _lib.last_launch("k_raster_fwd") == (1024, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_DEEP_FIRST | _lib.NR_LAUNCH_SPLIT)
     counts = _bin_candidates(proj[:4], f, 2 * s)
     assert counts.max() > 512, counts.max()  # deep bins: more than one 512-face staging round
     g = torch.randn(img.shape, generator=torch.Generator().manual_seed(43))

@@ -1020,13 +1020,15 @@ def test_renderer_camera_fit(dev):
     assert losses[-1] < 0.3 * losses[0], (losses[0], losses[-1])
 
 
-def test_hip_graph_capture_matches_eager(dev):
+@pytest.mark.parametrize("B,s,level", [(3, 64, 3), (8, 64, 4)])
+def test_hip_graph_capture_matches_eager(dev, B, s, level):
     """The fused forward + backward issues no host synchronisation (faces checks and adjacency are
     cached per tensor), so a whole step can be captured once in a HIP graph (torch.cuda.CUDAGraph)
     and replayed: the replayed images equal the eager ones bit for bit and the gradients agree
-    within the gradient tolerance (float atomics)."""
-    B, s = 3, 64
-    proj, f = _ico_batch(3, B, dev)
+    within the gradient tolerance (float atomics).  The second case is a split forward (deep bins at
+    1024 threads on the caller's stream, the rest at 256 on the library's side stream): the capture
+    records its fork and join."""
+    proj, f = _ico_batch(level, B, dev)
     faces = torch.as_tensor(f, device=dev)
     vt, ft, tex = nr.create_textures(f.shape[0], texture_size=4)
     tex = torch.as_tensor(np.random.RandomState(3).uniform(0, 1, tex.shape).astype(np.float32), device=dev)
@@ -1057,6 +1059,8 @@ def test_hip_graph_capture_matches_eager(dev):
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         img = step()
+    if B % 8 == 0:
+        assert _lib.last_launch("k_raster_fwd")[1] & _lib.NR_LAUNCH_SPLIT
     for _ in range(3):
         graph.replay()
     torch.cuda.synchronize()

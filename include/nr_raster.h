@@ -174,7 +174,9 @@ enum { NR_LIGHT_AMBIENT = 0, NR_LIGHT_DIRECTIONAL = 1, NR_LIGHT_SPECULAR = 2, NR
 /* Channels in output order: rgb (3), silhouettes (1), depth (1) -- those enabled by draw_flags. */
 NR_API int nr_num_channels(int draw_flags);
 
-/* rasterize.py:194-329 (without lights / backgrounds): images [B, C, s, s] contiguous. */
+/* rasterize.py:194-329 (without lights / backgrounds): images [B, C, s, s] contiguous.  Ordered on
+ * `stream`; a deep-bin batch (B % 8 == 0) forks part of the forward onto the library's side stream and
+ * joins it back with events before returning (NR_LAUNCH_SPLIT). */
 NR_API int nr_rasterize_forward(const NrRasterArgs* args, float* images, void* stream);
 
 /* Bytes of NrRasterArgs.textures_packed for texture_items textures of H x W texels. */

@@ -94,6 +94,10 @@ SideStream* side_stream(hipStream_t st) {
     static thread_local SideStream tab[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    // the side stream lives on the current device: a caller's stream of another device gets no split
+    hipDevice_t sdev = dev;
+    if (st && hipStreamGetDevice(st, &sdev) != hipSuccess) return nullptr;
+    if (sdev != dev) return nullptr;
     SideStream& x = tab[dev];
     if (!x.s) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

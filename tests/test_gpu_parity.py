@@ -360,6 +360,34 @@ def test_face_index_deep_stack_depth_cull(oracle_mod, dev, zlevels):
     assert (ref[1] >= 0).any() and (ref[1] < 0).any()
 
 
+def test_split_forward_capped_vs_oracle(oracle_mod, dev):
+    """The split forward (fused, anti-aliased, B % 8 == 0): every bin holds 1000+ candidates, so each
+    deep-first list's deep prefix is capped (a quarter of the items' bins may go to the 1024-thread
+    launch) and the remaining deep bins run in the 256-thread launch on the side stream, in its
+    multi-round static path; the face-index map is bit-exact against the oracle and the silhouette
+    and depth images match the ones the unsplit forward of the same faces gives item by item."""
+    r = np.random.RandomState(11)
+    S, F, B = 64, 4000, 16
+    cx = r.uniform(-0.9, 0.9, size=(B, F, 1))
+    cy = r.uniform(-0.9, 0.9, size=(B, F, 1))
+    x = (cx + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    y = (cy + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    z = r.uniform(0.5, 5.0, size=(B, F, 3)).astype(np.float32)
+    fg = np.stack([x, y, z], -1).astype(np.float32)
+    ref = oracle_mod.face_index_map(torch.as_tensor(fg), S)
+    verts = torch.as_tensor(fg.reshape(B, F * 3, 3), device=dev)
+    faces = torch.arange(F * 3, dtype=torch.int32, device=dev).reshape(F, 3)
+    hp = nr.RasterizeHyperparam(image_size=S // 2, anti_aliasing=True)
+    hp.draw_rgb = False
+    img, fim = nrr.rasterize_core(verts, faces, nr.RasterizeParam(), hp, return_face_index=True)
+    ntf, flags = _lib.last_launch("k_raster_fwd")
+    assert ntf == 1024 and flags & _lib.NR_LAUNCH_SPLIT, (ntf, flags)
+    assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
+    # items 0-7 alone: B % 8 == 0 still, but no cap (Bcap = 8 = B): the same images
+    img8, fim8 = nrr.rasterize_core(verts[:8].contiguous(), faces, nr.RasterizeParam(), hp, return_face_index=True)
+    assert torch.equal(fim8, fim[:8]) and torch.equal(img8, img[:8])
+
+
 def test_headline_properties(dev):
     """Full headline config (B=64, 256^2 AA, ico 5120, rgb+sil+depth): size-independent properties."""
     B = 64

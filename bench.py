@@ -515,8 +515,8 @@ def main():
     fracs = {"hbm": hbm_frac}
     if valu is not None:
         fracs["valu"] = valu["frac"]
-    bound = max(fracs, key=fracs.get)
-    limiter = bound if fracs[bound] >= 0.6 else "latency"
+    closest = max(fracs, key=fracs.get)
+    limiter = closest if fracs[closest] >= 0.6 else "latency"
 
     res = {
         "metric": "rasterize Mpixels/s fwd+bwd, 256² batch=64; % HBM roofline at 1 & 8 GPU",
@@ -538,7 +538,9 @@ def main():
                    "channels": w["C"], "parallelism": "batch-sharded dp%d" % world},
         "host_ms_per_step": round(host_elapsed / args.steps * 1e3, 4),
         "host_ms_per_step_autograd_single_thread": round(host_single, 4),
-        "roofline": {"bound": bound, "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+        # achieved / peak / frac are against the HBM roof (the contract's "bound"); the VALU roof beside
+        # it, the closer of the two, and what limits the kernel
+        "roofline": {"bound": "hbm", "closest_roof": closest, "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(hbm_frac, 5), "traffic": traffic,
                      "traffic_source": pmc_note, "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 5),
                      "copy_ceiling_gbs": round(ceiling, 1),

@@ -8,8 +8,10 @@ One step = rasterize_core forward + backward with a fixed N(0,1) upstream gradie
 of (images * G).sum()), producing d/dvertices and d/dtextures.
 
 Multi-GPU: one process per GPU, each renders its own 64 items (batch sharding, weak scaling, no
-collective on the data path); the timed region is bracketed by barriers and the max over ranks is
-reported.  Under torchrun the ranks come from its environment; `bench.py --gpus N` started without
+collective on the image data path).  The texture atlas is one parameter shared by every item of
+every rank, so each timed step ends with the all_reduce(SUM) of its gradient over the ranks (SURVEY
+section 8e; also timed on its own as allreduce_ms).  The timed region is bracketed by barriers and
+the max over ranks is reported.  Under torchrun the ranks come from its environment; `bench.py --gpus N` started without
 a launcher spawns the N rank processes itself (before any GPU call) and exits with their status.
 The launched world size must equal --gpus (exit status 2 otherwise).  With N > 1 the rank images
 are then all-gathered over RCCL (BASELINE cfg4: 512 items on 8 GPUs "with RCCL gather") and that
@@ -156,16 +158,26 @@ def workload(args, rank, dev):
     g = torch.as_tensor(np.random.RandomState(7).normal(size=(B, C, args.image_size, args.image_size))
                         .astype(np.float32), device=dev)
     return dict(nr=nr, proj=proj, faces=faces, params=params, hp=hp, tex=tex, g=g, C=C, V=v.shape[0],
-                F=f.shape[0], tex_shape=None if tex is None else tuple(tex.shape))
+                F=f.shape[0], tex_shape=None if tex is None else tuple(tex.shape),
+                # parameters every rank's items share: their gradient is summed over the ranks inside
+                # the step; the projected vertices are per item, no exchange
+                shared=[] if tex is None else [tex])
 
 
 def step(w):
+    """One step: rasterize_core forward + backward of this rank's items and, with more than one
+    rank, the all_reduce(SUM) of the shared texture atlas's gradient (every item samples the same
+    atlas, so its gradient is the reference's index_put_ scatter summed over the whole global batch,
+    rasterize.py:144-148, utils.py:104-114; distributed.allreduce_shared_grads)."""
     from neural_renderer_v2_pytorch_amd.rasterize import rasterize_core
+    from neural_renderer_v2_pytorch_amd import distributed
     w["proj"].grad = None
     if w["tex"] is not None:
         w["tex"].grad = None
     images = rasterize_core(w["proj"], w["faces"], w["params"](), w["hp"])
     images.backward(w["g"])
+    if w["shared"]:
+        distributed.allreduce_shared_grads(w["shared"])  # no-op without a process group of > 1 rank
     return images
 
 
@@ -211,6 +223,9 @@ def kernel_bytes(w, args, measured=None):
             k["k_raster_fwd"] += k.pop("k_shade") - fim
         if "k_tex_pack" not in measured:
             k["k_face_setup"] += k.pop("k_tex_pack")
+        if rgb and "k_tex_out" not in measured and "k_vertex_grad" in measured:
+            # the texture-gradient output carried by k_vertex_grad's blocks (small enough textures)
+            k["k_vertex_grad"] += k.pop("k_tex_out")
     total = B * (8 * S * S + 8 * C * s * s + 36 * V) + 24 * F + (2 * T if T else 0)
     return k, total
 
@@ -422,6 +437,23 @@ def main():
     px = world * args.batch * args.image_size ** 2 * args.steps
     value = px / elapsed / 1e6
 
+    # the shared-gradient all_reduce that every timed step above includes, timed on its own (one
+    # warm-up was the steps', then the best of 3, max over ranks), like gather_ms below
+    allreduce_ms = None
+    if world > 1 and w["shared"]:
+        from neural_renderer_v2_pytorch_amd import distributed
+        times = []
+        for _ in range(3):
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            distributed.allreduce_shared_grads(w["shared"])
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t1) * 1e3)
+        t = torch.tensor([min(times)], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        allreduce_ms = float(t.item())
+
     gather_ms = None
     if not args.no_gather and world > 1:
         out = torch.empty((world * images.shape[0],) + tuple(images.shape[1:]), device=dev, dtype=images.dtype)
@@ -559,6 +591,10 @@ def main():
         # the same step replayed from a captured HIP graph (not the headline value)
         res["graph_ms_per_step"] = round(graph_ms, 4)
         res["graph_value"] = round(world * args.batch * args.image_size ** 2 / (graph_ms * 1e-3) / 1e6, 3)
+    if allreduce_ms is not None:
+        # inside every timed step (ms_per_step includes it); the bytes it sums per rank
+        res["allreduce_ms"] = round(allreduce_ms, 4)
+        res["allreduce_bytes"] = int(sum(p.numel() * p.element_size() for p in w["shared"]))
     if gather_ms is not None:
         res["gather_ms"] = round(gather_ms, 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

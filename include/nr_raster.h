@@ -199,7 +199,8 @@ NR_API size_t nr_backward_workspace_bytes(int batch_size, int num_faces, int num
  * (the forward zeroed them through NrRasterArgs.bwd_workspace and no backward has used it since):
  * the backward then skips its own zero fill; 0 = the backward zero-fills (always correct).  With 1,
  * args->bwd_workspace must be `workspace` and args->bwd_workspace_bytes must cover the accumulators
- * (NR_ERR_ARGS otherwise).  A second backward over the same forward state must pass 0. */
+ * (NR_ERR_ARGS otherwise).  A second backward over the same forward state must pass 0.  A texture
+ * gradient takes at most 2^25 texels per texture and rows of at most 2^22 - 1 texels (NR_ERR_ARGS). */
 NR_API int nr_rasterize_backward(const NrRasterArgs* args, const float* grad_images, float* grad_vertices,
                                  float* grad_textures, void* workspace, size_t workspace_bytes, int workspace_zeroed,
                                  void* stream);

@@ -833,13 +833,13 @@ void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, con
     const bool one = (long long)grid.x * grid.y < 8192;
     if (one) {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
-        g_last_bwd = LaunchRec{2 * NT, 0};
+        g_last_bwd.store(LaunchRec{2 * NT, 0});
     } else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2) {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC>), grid, dim3(NT), 0, st, ba, g, sh);
-        g_last_bwd = LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE};
+        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE});
     } else {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
-        g_last_bwd = LaunchRec{NT, NR_LAUNCH_TWO_PX_PER_LANE};
+        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_TWO_PX_PER_LANE});
     }
 }
 

@@ -55,11 +55,23 @@ bool g_prof_rec[P_N];
 
 // launch record (nr_last_launch): block size and NR_LAUNCH_* flags of the latest raster launches in
 // this process (process-wide: torch runs a backward on its autograd device thread), so tests can
-// assert the variant that actually ran
+// assert the variant that actually ran.  One 64-bit word per kernel, stored and loaded with relaxed
+// atomics: a reader sees one whole record; with several threads rendering at once it is one of
+// their latest, not a particular thread's (a diagnostic)
 struct LaunchRec {
     int threads = 0, flags = 0;
 };
-LaunchRec g_last_fwd, g_last_bwd;
+struct LaunchSlot {
+    unsigned long long w = 0;
+    void store(LaunchRec r) {
+        __atomic_store_n(&w, ((unsigned long long)(unsigned)r.flags << 32) | (unsigned)r.threads, __ATOMIC_RELAXED);
+    }
+    LaunchRec load() const {
+        const unsigned long long v = __atomic_load_n(&w, __ATOMIC_RELAXED);
+        return LaunchRec{(int)(unsigned)(v & 0xffffffffu), (int)(unsigned)(v >> 32)};
+    }
+};
+LaunchSlot g_last_fwd, g_last_bwd;
 
 struct ProfScope {  // records the start/end events of one launch when profiling is on
     int k;

@@ -515,11 +515,14 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
 constexpr long long NR_FTIMING_MAX = 1 << 22;
 constexpr int NR_FTSLOTS = 10;  // per wave: 8 phase slots, then the wall clock (100 MHz, chip-wide) at start and end
 __device__ unsigned long long g_fwd_t[NR_FTIMING_MAX];
+// (k_raster_fwd only: a split forward's second launch, part 2, writes the upper half of the buffer, so
+// the two launches' stamps do not overlap; tools/fwd_timing.py decodes each with its own block size)
 #define NR_FTSTAMP(k, v)                                                                                   \
     do {                                                                                                   \
+        const long long h_ = NR_FTIMING_MAX / 2;                                                           \
         const long long i_ = (((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * NR_FTSLOTS + (k); \
         const unsigned long long t_ = (v);                                                                 \
-        if ((threadIdx.x & 63) == 0 && i_ < NR_FTIMING_MAX) g_fwd_t[i_] = t_;                       \
+        if ((threadIdx.x & 63) == 0 && i_ < h_) g_fwd_t[i_ + (part == 2 ? h_ : 0)] = t_;                  \
     } while (0)
 #else
 #define NR_FTSTAMP(k, v) \

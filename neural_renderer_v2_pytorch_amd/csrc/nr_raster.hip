@@ -81,17 +81,34 @@ size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
 }
 
 // A side stream per (host thread, device) for the split forward, with its fork / join events; created
-// on first use outside a stream capture (null: no split for this call)
+// on first use outside a stream capture (null: no split for this call).  The thread's table releases
+// them when the thread ends (a worker pool's recycled threads do not accumulate streams); the streams
+// are synchronised first, so work still queued on one finishes before it is destroyed.
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+};
+struct SideStreamTable {
+    SideStream tab[64];
+    ~SideStreamTable() {
+        for (SideStream& x : tab) {
+            if (x.s) {
+                (void)hipStreamSynchronize(x.s);
+                (void)hipStreamDestroy(x.s);
+            }
+            if (x.fork) (void)hipEventDestroy(x.fork);
+            if (x.join) (void)hipEventDestroy(x.join);
+            x = SideStream{};
+        }
+    }
 };
 #ifndef NR_SPLIT_BUCKET
 #define NR_SPLIT_BUCKET 10
 #endif
 constexpr int SPLIT_BUCKET = NR_SPLIT_BUCKET;  // deep bins: >= 512 candidates
 SideStream* side_stream(hipStream_t st) {
-    static thread_local SideStream tab[64];
+    static thread_local SideStreamTable table;
+    SideStream* tab = table.tab;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
     // the side stream lives on the current device: a caller's stream of another device gets no split
@@ -105,7 +122,9 @@ SideStream* side_stream(hipStream_t st) {
         if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess ||
             hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) {
-            x.s = nullptr;
+            if (x.fork) (void)hipEventDestroy(x.fork);
+            if (x.join) (void)hipEventDestroy(x.join);
+            x = SideStream{};
             return nullptr;
         }
     }
@@ -208,9 +227,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     {
         ProfScope _p(P_RASTER, st);
         const int rs = vertices ? FACE_REC : 9;
-        g_last_fwd = LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
-                               (fuse && ntf == 256 && sh.C == MAXC ? NR_LAUNCH_STATIC_CHANNELS : 0) |
-                               (ordered ? NR_LAUNCH_DEEP_FIRST : 0) | (side ? NR_LAUNCH_SPLIT : 0)};
+        g_last_fwd.store(LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
+                                        (fuse && ntf == 256 && sh.C == MAXC ? NR_LAUNCH_STATIC_CHANNELS : 0) |
+                                        (ordered ? NR_LAUNCH_DEEP_FIRST : 0) | (side ? NR_LAUNCH_SPLIT : 0)});
         if (side) {
             // fork: the side stream waits for the setup and the order; join: the caller's stream waits
             // for the side stream's launch
@@ -401,9 +420,11 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     const bool lit = (a->draw_flags & NR_DRAW_RGB) && a->num_lights > 0;
     const int tex_items = rgb ? (a->tex_stride_b ? a->batch_size : 1) : 0;
     // texel indices of the backward's direct samples ride in a 32-bit field (nr_bwd.h POS_DIRECT)
-    if (rgb && (long long)a->tex_height * a->tex_width > DIRECT_MAX_HW)
-        return fail(NR_ERR_ARGS, "texture gradient: at most %d texels per texture (got %d x %d)", DIRECT_MAX_HW,
-                    a->tex_height, a->tex_width);
+    // (and a row at most DIRECT_OFF - 1 texels wide: the top-left index of a sample one row above the
+    // texture, -W - 1 + x, must stay above -DIRECT_OFF to be encoded)
+    if (rgb && ((long long)a->tex_height * a->tex_width > DIRECT_MAX_HW || a->tex_width >= DIRECT_OFF))
+        return fail(NR_ERR_ARGS, "texture gradient: at most %d texels per texture and %d per row (got %d x %d)",
+                    DIRECT_MAX_HW, DIRECT_OFF - 1, a->tex_height, a->tex_width);
     const size_t need = nr_backward_workspace_bytes(a->batch_size, a->num_faces, a->num_vertices, tex_items,
                                                     a->tex_height, a->tex_width, lit ? a->num_lights : 0);
     if (need > 0 && (!workspace || workspace_bytes < need))
@@ -654,12 +675,13 @@ __attribute__((visibility("default"))) int nr_debug_bwd_timing(unsigned long lon
 
 int nr_last_launch(const char* kernel, int* block_threads, int* flags) {
     if (!kernel || !block_threads || !flags) return fail(NR_ERR_ARGS, "null argument");
-    const LaunchRec* r = strcmp(kernel, "k_raster_fwd") == 0 ? &g_last_fwd
-                         : strcmp(kernel, "k_raster_bwd") == 0 ? &g_last_bwd : nullptr;
-    if (!r) return fail(NR_ERR_ARGS, "nr_last_launch: unknown kernel name %s", kernel);
-    if (!r->threads) return fail(NR_ERR_ARGS, "nr_last_launch: no %s launch recorded on this thread", kernel);
-    *block_threads = r->threads;
-    *flags = r->flags;
+    const LaunchSlot* slot = strcmp(kernel, "k_raster_fwd") == 0 ? &g_last_fwd
+                             : strcmp(kernel, "k_raster_bwd") == 0 ? &g_last_bwd : nullptr;
+    if (!slot) return fail(NR_ERR_ARGS, "nr_last_launch: unknown kernel name %s", kernel);
+    const LaunchRec r = slot->load();
+    if (!r.threads) return fail(NR_ERR_ARGS, "nr_last_launch: no %s launch recorded in this process", kernel);
+    *block_threads = r.threads;
+    *flags = r.flags;
     return NR_OK;
 }
 

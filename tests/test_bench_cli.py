@@ -49,4 +49,7 @@ def test_bench_cli_two_ranks_gloo():
     assert res["config"]["global_batch"] == 128
     assert res["config"]["parallelism"] == "batch-sharded dp2"
     assert res["gather_ms"] is not None and res["gather_ms"] > 0
+    # the shared texture gradient's all_reduce is part of every timed step, and timed on its own
+    assert res["allreduce_ms"] is not None and res["allreduce_ms"] > 0
+    assert res["allreduce_bytes"] == 3 * 288 * 288 * 4
     assert res["value"] > 0 and res["steps"] == 3

@@ -101,3 +101,60 @@ def test_world2_hip_path_matches_full_batch(tmp_path, dev, batch):
         assert np.array_equal(got["images_known"], want), "rank %d gathered images (known batch)" % r
         _close(got["grad_mesh"], mesh.grad.cpu().numpy(), "rank %d shared mesh gradient" % r)
         _close(got["grad_atlas"], atlas.grad.cpu().numpy(), "rank %d shared texture gradient" % r)
+
+
+def _bench_args(batch):
+    import argparse
+    return argparse.Namespace(batch=batch, level=4, image_size=256, mode="rgbsd")
+
+
+def _bench_worker(rank, world_size, port, out_dir):
+    """One rank of bench.py's N > 1 step: its own 64 headline items, forward + backward, then the
+    all_reduce of the shared atlas gradient that bench.step issues inside the timed region."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        import bench
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        w = bench.workload(_bench_args(64), rank, dev)
+        assert w["shared"] == [w["tex"]]
+        bench.step(w)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, "b%d.npz" % rank), grad_atlas=w["tex"].grad.cpu().numpy(),
+                 grad_proj=w["proj"].grad.cpu().numpy(), g=w["g"].cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_step_allreduce_matches_128_items(tmp_path, dev):
+    """bench.py's N > 1 step is the whole sharded step: two gloo ranks, 64 headline items each
+    (bench.workload: items 0-63 and 64-127, one shared 288^2 atlas), each ending its step with the
+    all_reduce(SUM) of the atlas gradient.  Both ranks' atlas gradients must equal the gradient of
+    the same 128 items rendered and differentiated in one process (the reference's index_put_
+    scatter summed over the global batch, rasterize.py:144-148, utils.py:104-114) within
+    GRAD_TOL; each rank's projected-vertex gradients equal that process's for its items."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    mp.spawn(_bench_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = [np.load(str(tmp_path / ("b%d.npz" % r))) for r in range(2)]
+    w = bench.workload(_bench_args(128), 0, dev)
+    # bench.workload draws each rank's upstream gradient from the same seed: the 128-item run uses
+    # the two ranks' gradients side by side
+    w["g"] = torch.as_tensor(np.concatenate([got[0]["g"], got[1]["g"]]), device=dev)
+    bench.step(w)  # no process group here: no all_reduce, one batched backward over 128 items
+    want_atlas = w["tex"].grad.cpu().numpy()
+    want_proj = w["proj"].grad.cpu().numpy()
+    assert float(np.abs(want_atlas).sum()) > 0
+    for r in range(2):
+        _close(got[r]["grad_atlas"], want_atlas, "rank %d all-reduced atlas gradient" % r)
+        _close(got[r]["grad_proj"], want_proj[64 * r:64 * (r + 1)], "rank %d projected-vertex gradient" % r)
+    # a rank's own (un-reduced) gradient is not the global one: the all_reduce did the work
+    single = bench.workload(_bench_args(64), 0, dev)
+    bench.step(single)
+    part = single["tex"].grad.cpu().numpy()
+    assert np.abs(part - want_atlas).max() > 1e-2 * np.abs(want_atlas).max()

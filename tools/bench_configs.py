@@ -14,7 +14,11 @@ cfg2 is also timed as a HIP-graph replay of the captured step (graph_ms_per_step
 step is bound by host launch overhead, not by the kernels.
 cfg1 is the reference's CPU-only plumbing case and cfg4 is bench.py --gpus 8.
 
-usage: python tools/bench_configs.py [--steps 20] [--warmup 5] [--loop-steps 200]
+Each line carries a per-config roofline (algorithmic bytes per kernel and step with the config's real
+texture size, HBM fraction per kernel and per step) and, with --pmc, each kernel's measured HBM
+traffic and its ratio to the algorithmic bytes.
+
+usage: python tools/bench_configs.py [--steps 20] [--warmup 5] [--loop-steps 200] [--pmc]
 """
 import argparse
 import json
@@ -106,7 +110,7 @@ def scene(v, f, B, dev, seed=0):
     return synthetic.project(vb.to(dev), eyes.to(dev)).contiguous().detach().requires_grad_(True)
 
 
-def cfg2(dev, a):
+def cfg2_step(dev):
     v, f = nr.load_obj(os.path.join(DATA, "teapot.obj"))
     B, s = 4, 256
     proj = scene(v, f, B, dev)
@@ -123,6 +127,13 @@ def cfg2(dev, a):
         params = nr.RasterizeParam(vertices_textures=vt_d[None].expand(B, -1, -1), faces_textures=ft_d,
                                    textures=tex[None].expand(B, -1, -1, -1))
         nr.rasterize_core(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
+    meta = dict(batch=B, image_size=s, C=5, V=int(v.shape[0]), F=int(f.shape[0]), tex_shape=tuple(tex.shape))
+    return step, meta
+
+
+def cfg2(dev, a):
+    step, m = cfg2_step(dev)
+    B, s = m["batch"], m["image_size"]
     t = pipelined_step(step, a.steps, a.warmup)
     ts = median_step(step, a.steps, a.warmup)
     # the same eager steps with the autograd engine in the calling thread (a user-side setting that
@@ -130,15 +141,15 @@ def cfg2(dev, a):
     with torch.autograd.set_multithreading_enabled(False):
         t1 = pipelined_step(step, a.steps, a.warmup)
         t1s = median_step(step, a.steps, a.warmup)
-    res = dict(config="cfg2 teapot B=4 256^2 rgb+sil+depth", faces=int(f.shape[0]), batch=B, image_size=s,
+    res = dict(config="cfg2 teapot B=4 256^2 rgb+sil+depth", faces=m["F"], batch=B, image_size=s,
                ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
                synced_ms_per_step=round(ts * 1e3, 4),
                single_thread_autograd_ms_per_step=round(t1 * 1e3, 4),
                single_thread_autograd_synced_ms_per_step=round(t1s * 1e3, 4),
                kernels_ms=kernels_ms(step))
-    proj.grad = tex.grad = None
     tg = median_step(graphed(step), a.steps, a.warmup)
     res.update(graph_ms_per_step=round(tg * 1e3, 4), graph_mpx_per_s=round(B * s * s / tg / 1e6, 1))
+    res["roofline"] = roofline(m, res["kernels_ms"], tg * 1e3, "graph_ms_per_step")
     return res
 
 
@@ -161,6 +172,7 @@ def cfg3_step(dev):
     def step():
         proj.grad = tex.grad = None
         nr.rasterize_rgba(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
+    step.meta = dict(batch=B, image_size=s, C=4, V=int(v.shape[0]), F=int(f.shape[0]), tex_shape=tuple(tex.shape))
     return step, f, B, s
 
 
@@ -168,12 +180,14 @@ def cfg3(dev, a):
     step, f, B, s = cfg3_step(dev)
     t = pipelined_step(step, a.steps, a.warmup)
     ts = median_step(step, a.steps, a.warmup)
-    return dict(config="cfg3 car (1x subdivided) B=64 256^2 textured rgba", faces=int(f.shape[0]), batch=B,
-                image_size=s, ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
-                synced_ms_per_step=round(ts * 1e3, 4), kernels_ms=kernels_ms(step))
+    res = dict(config="cfg3 car (1x subdivided) B=64 256^2 textured rgba", faces=int(f.shape[0]), batch=B,
+               image_size=s, ms_per_step=round(t * 1e3, 4), mpx_per_s=round(B * s * s / t / 1e6, 1),
+               synced_ms_per_step=round(ts * 1e3, 4), kernels_ms=kernels_ms(step))
+    res["roofline"] = roofline(step.meta, res["kernels_ms"], t * 1e3, "ms_per_step")
+    return res
 
 
-def cfg5(dev, a):
+def cfg5_step(dev):
     v, f = synthetic.torus(250, 100)
     s = 512
     faces = torch.as_tensor(f, device=dev)
@@ -190,6 +204,12 @@ def cfg5(dev, a):
         loss = ((ren.render_silhouettes(verts, faces) - target) ** 2).sum()
         loss.backward()
         opt.step()
+    step.meta = dict(batch=1, image_size=s, C=1, V=int(v.shape[0]), F=int(f.shape[0]), tex_shape=None)
+    return step, v, f, s, faces, ren, target, verts
+
+
+def cfg5(dev, a):
+    step, v, f, s, faces, ren, target, verts = cfg5_step(dev)
     t = pipelined_step(step, a.steps, a.warmup)
     ts = median_step(step, a.steps, a.warmup)
     torch.cuda.synchronize()
@@ -220,7 +240,65 @@ def cfg5(dev, a):
         replay()
     torch.cuda.synchronize()
     res.update(graph_ms_per_step=round(tg * 1e3, 4), graph_loop_s=round(time.perf_counter() - t0, 4))
+    # the step's rasterizer part only (the Adam update, loss and camera are torch's / the camera kernels')
+    res["roofline"] = roofline(step.meta, res["kernels_ms"], tg * 1e3, "graph_ms_per_step (incl. Adam, loss, camera)")
     return res
+
+
+def roofline(meta, kms, step_ms, step_from):
+    """Per-config roofline: each kernel's algorithmic (compulsory) HBM bytes per
+    launch (bench.kernel_bytes, the formulas of DESIGN.md section 4, with this config's real texture
+    size: the car's atlas is 3 x 1190 x 1920 f32 = 27.4 MB) over its HIP-event time, against the 8 TB/s
+    HBM roof; and the whole step's bytes B(8S^2 + 8Cs^2 + 36V) + 24F + 2T over the step time."""
+    import argparse
+    import bench
+    w = dict(C=meta["C"], V=meta["V"], F=meta["F"], tex_shape=meta["tex_shape"])
+    args = argparse.Namespace(batch=meta["batch"], image_size=meta["image_size"])
+    kb, total = bench.kernel_bytes(w, args, kms)
+    per = {}
+    for k, ms in kms.items():
+        if k in kb:
+            per[k] = dict(ms=ms, algorithmic_bytes=int(kb[k]),
+                          frac=round(kb[k] / (ms * 1e-3) / 1e9 / bench.HBM_PEAK_GBS, 5))
+    T = 0 if meta["tex_shape"] is None else 3 * meta["tex_shape"][1] * meta["tex_shape"][2] * 4
+    return dict(peak_gbs=bench.HBM_PEAK_GBS, texture_bytes=T, kernels=per, step_algorithmic_bytes=int(total),
+                step_ms=round(step_ms, 4), step_from=step_from,
+                step_frac=round(total / (step_ms * 1e-3) / 1e9 / bench.HBM_PEAK_GBS, 5))
+
+
+def pmc_child(name, steps=3):
+    """One profiled pass (under rocprofv3 --pmc): `steps` steps of config `name`, then bench.py's 1 GiB
+    calibration stream of known byte count (tools/pmc_traffic.py scales the counters with it)."""
+    import bench
+    dev = torch.device("cuda", 0)
+    step = {"cfg2": lambda: cfg2_step(dev)[0], "cfg3": lambda: cfg3_step(dev)[0],
+            "cfg5": lambda: cfg5_step(dev)[0]}[name]()
+    for _ in range(steps + 1):
+        step()
+    torch.cuda.synchronize()
+    bench.copy_ceiling_gbs(dev)
+    torch.cuda.synchronize()
+
+
+def pmc_traffic(name, timeout_s=240):
+    """HBM bytes per launch of each kernel of config `name`: FETCH_SIZE and WRITE_SIZE, each in a
+    rocprofv3 --pmc pass of its own over a child process (pmc_child), as bench.py's in-run passes."""
+    import shutil
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_traffic as pt
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    d = tempfile.mkdtemp(prefix="nr_cfg_pmc_")
+    try:
+        for i, counter in enumerate(("FETCH_SIZE", "WRITE_SIZE"), 1):
+            cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", os.path.join(d, "p%d" % i), "-o", "run",
+                   "--", sys.executable, os.path.abspath(__file__), "--pmc-child", name]
+            subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout_s, check=True,
+                           cwd=ROOT, env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+        return pt.summarize(d, [name], verbose=False)["hbm_bytes_per_launch"]
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def main():
@@ -232,10 +310,26 @@ def main():
     p.add_argument("--calibrate", action="store_true",
                    help="end with bench.py's 1 GiB copy stream (the FETCH_SIZE / WRITE_SIZE calibration of "
                         "tools/pmc_traffic.py when this runs under rocprofv3 --pmc)")
+    p.add_argument("--pmc", action="store_true",
+                   help="add each config's PMC traffic per kernel (two rocprofv3 --pmc passes per config) and its "
+                        "ratio to the algorithmic bytes")
+    p.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)  # one profiled pass (internal)
     a = p.parse_args()
+    if a.pmc_child:
+        return pmc_child(a.pmc_child)
     dev = torch.device("cuda", 0)
     for name in a.only.split(","):
         r = globals()[name](dev, a)
+        if a.pmc:
+            try:
+                tr = pmc_traffic(name)
+                for k, kr in r["roofline"]["kernels"].items():
+                    if k in tr:
+                        kr["traffic"] = tr[k]
+                        kr["traffic_ratio"] = round(tr[k] / kr["algorithmic_bytes"], 3)
+                r["roofline"]["traffic_source"] = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, calibrated on a 1 GiB stream"
+            except Exception as e:  # a profiler failure must not lose the timing line
+                r["roofline"]["traffic_source"] = "pmc passes failed: %r" % (e,)
         print(json.dumps(r), flush=True)
     if a.calibrate:
         import bench

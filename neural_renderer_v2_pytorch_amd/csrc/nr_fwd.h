@@ -537,7 +537,7 @@ constexpr int FWD_WPE = 8;
 // map is not read back and k_shade has no launch of its own.
 // CC (SHADE only): the channel count as a compile-time constant; CC = MAXC means rgb + sil + depth,
 // so the epilogue's draw-flag tests and per-channel guards fold away (0: sh.C / sh.draw at run time)
-template <int NTF, bool SHADE, int CC = 0>
+template <int NTF, bool SHADE, int CC = 0, bool XCULL = false>
 __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
@@ -548,7 +548,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
-    constexpr bool CULL = NTF == 1024;  // deep bins: small faces over each 8x8 block
+    // deep bins: small faces over each 8x8 block (XCULL: the 256-thread variant too, for a split
+    // forward's shallow bins)
+    constexpr bool CULL = NTF == 1024 || XCULL;
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
     __shared__ int s_scan[C::NW];
     __shared__ int s_next;  // (dyn) next 8x8 block to walk

@@ -331,7 +331,8 @@ template <int NTF> struct FwdCfg {
     static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
     static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
     static constexpr int FCAP = NTF >= 1024 ? 512 : 160;       // faces staged per round
-    static constexpr int LDS = FCAP * FREC * 16 + CAND * 4;
+    // staged records, candidate ids (dyn + SHADE: then the winners' staging slots), block masks
+    static constexpr int LDS = FCAP * FREC * 16 + CAND * 4 + FCAP * 2 + 16 * 4;
     // 8x8 block k of wave w: its origin (ox, oy) in the bin
     __device__ static __forceinline__ void block_of(int w, int k, int& ox, int& oy) {
         if (NSUB == 1) {         // 16 waves: wave w owns block (w & 3, w >> 2)
@@ -417,41 +418,37 @@ __device__ __forceinline__ void face_commit(const float4* s_face, int slot, floa
     }
 }
 
-// Edge cull of a staged face against an 8x8 block (deep-bin variant): true only when the reference's
-// edge tests (.cu:107-116) fail at every pixel centre of the block (nr_cull.h)
-template <int FST>
-__device__ __forceinline__ bool block_culled(const float4* e, float xc, float yc, float hx, float hy) {
-    const float4 q2 = e[2 * FST], q3 = e[3 * FST], q4 = e[4 * FST];
-    // x0 y0 x1 y1 x2 y2 A B C D E F
-    return nr_block_culled(q2.z, q2.x, q4.y, q4.x, q2.w, q2.y, q3.x, q3.z, q4.z, q4.w, q3.y, q3.w, xc, yc, hx, hy);
-}
-
 constexpr int ZCULL_MIN = 512;  // candidates of a bin (first bin-mask round)
-// one wave's walk of the n staged faces over its 8x8 block (pixel (xp, yp) per lane, pixel-centre
-// extent [xc0, xc1] x [yc0, yc1]): bbox ballot (+ edge cull), then the per-face test in ascending order
-template <int FST, bool CULL, bool SLOT, bool ZCULL = false>
-__device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, int n, int lane, float xp, float yp,
-                                           float xc0, float xc1, float yc0, float yc1, float near, float far,
-                                           float delta, float& depth_min, int& best) {
+#ifndef NR_ZREFRESH
+#define NR_ZREFRESH 255
+#endif
+// one wave's walk of the n staged faces over its 8x8 block u of the bin (pixel (xp, yp) per lane): the
+// ballot takes the staged faces whose block mask (face_block_mask: bbox, and with CULL the edge cull)
+// has bit u, then the per-face test runs in ascending order
+template <int FST, bool SLOT, bool ZCULL = false>
+__device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, const uint16_t* __restrict__ s_bm, int u,
+                                           int n, int lane, float xp, float yp, float near, float far, float delta,
+                                           float& depth_min, int& best) {
     int pend = -1;               // staging slot of my pixel's pending face
     unsigned long long occ = 0;  // the wave's pixels with a pending face
     // (ZCULL: the deep variant's bins of >= ZCULL_MIN candidates) a face whose nearest corner lies
-    // behind every pixel's current depth (the wave's maximum, refreshed every 256 faces) fails the pass
-    // test's depth reject at each of them (depth_min only decreases; NaN bounds are kept): it is
-    // dropped in the ballot, with 63 others, instead of walked alone.  Car forward 0.625 -> 0.601 ms;
-    // the 50k torus (deep bins of low depth complexity) 0.118 -> 0.120 ms; on every bin of the headline
-    // and the torus the gate-free version cost +4 us each (same-box A/Bs, gpurun_out/o4-o9).
+    // behind every pixel's current depth (the wave's maximum, refreshed when a commit has changed a
+    // depth since, at most every NR_ZREFRESH + 1 faces) fails the pass test's depth reject at each of
+    // them (depth_min only decreases; NaN bounds are kept): it is dropped in the ballot, with 63
+    // others, instead of walked alone.  Car forward 0.625 -> 0.601 ms; the 50k torus (deep bins of low
+    // depth complexity) 0.118 -> 0.120 ms; on every bin of the headline and the torus the gate-free
+    // version cost +4 us each (same-box A/Bs, gpurun_out/o4-o9).
     float zmax = 0.f;
+    bool dirty = true;  // (wave-uniform) a commit may have lowered a depth since zmax was taken
     for (int c0 = 0; c0 < n; c0 += 64) {
-        if (ZCULL && (c0 & 255) == 0) zmax = wave_max(depth_min);  // refreshed every 256 faces
+        if (ZCULL && dirty && (c0 & NR_ZREFRESH) == 0) {
+            zmax = wave_max(depth_min);
+            dirty = false;
+        }
         bool hit = false;
         if (c0 + lane < n) {
-            const float4 q0 = s_face[c0 + lane];
-            hit = !(xc1 < q0.x || xc0 > q0.y || yc1 < q0.z || yc0 > q0.w);
+            hit = (s_bm[c0 + lane] >> u) & 1;
             if (ZCULL) hit = hit && !(s_face[FST + c0 + lane].x > zmax);
-            if (CULL && hit)
-                hit = !block_culled<FST>(s_face + c0 + lane, 0.5f * (xc0 + xc1), 0.5f * (yc0 + yc1), 0.5f * (xc1 - xc0),
-                                         0.5f * (yc1 - yc0));
         }
         // faces touching this wave's pixels, walked in ascending order
         for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
@@ -482,6 +479,7 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
                 if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
                 pend = -1;
                 occ = 0;
+                dirty = true;
             }
             {
                 int sv = slot;
@@ -493,12 +491,63 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, in
     if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
 }
 
-template <int FST>
-__device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ c, int f) {
+// Which of the bin's sixteen 8x8 pixel blocks a staged face may touch: bit 4 r + j (block column j, row
+// r of the 32x32 bin at (bx0, by0)) is set when the face's float bbox meets the block's pixel-centre
+// extent [pix_center(bx0 + 8 j), pix_center(bx0 + 8 j + 7)] x (the same in y) and, with CULL, its
+// edges do not fail at every pixel centre of the block (nr_block_culled) -- the predicate each wave's
+// ballot used to evaluate per 8x8 block and 64 staged faces, with the same float operations, so the
+// walked faces are the same.  Evaluated once per staged face, by its staging lane, which takes its
+// face's overlapped blocks one at a time: the edge cull runs once per (face, overlapped block) pair
+// instead of once per (wave, 64 staged faces), where most of the 64 lanes had no overlap to test.
+template <bool CULL>
+__device__ __forceinline__ uint32_t face_block_mask(float x0, float y0, float x1, float y1, float x2, float y2,
+                                                    float xmin, float xmax, float ymin, float ymax,
+                                                    const float* __restrict__ ext, int r0, int nr) {
+    // ext: the blocks' pixel-centre extents, [0..3] x lo, [4..7] x hi, [8..11] y lo, [12..15] y hi per
+    // block column / row (block_extents, in LDS: computed once per bin, read as broadcasts); only the
+    // block rows r0 .. r0 + nr - 1 are evaluated (the deep variant splits a face's rows over two lanes)
+    uint32_t mx = 0, m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) mx |= (!(ext[4 + j] < xmin || ext[j] > xmax) ? 1u : 0u) << j;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        if (r >= r0 && r < r0 + nr) m |= !(ext[12 + r] < ymin || ext[8 + r] > ymax) ? mx << (4 * r) : 0u;
+    if (CULL) {
+        const float A = x1 - x0, B = y1 - y0, C = x2 - x1, D = y2 - y1, E = x0 - x2, F = y0 - y2;
+        for (uint32_t rest = m; rest; rest &= rest - 1) {
+            const int u = __builtin_ctz(rest), j = u & 3, r = u >> 2;
+            const float xl = ext[j], xh = ext[4 + j], yl = ext[8 + r], yh = ext[12 + r];
+            if (nr_block_culled(x0, y0, x1, y1, x2, y2, A, B, C, D, E, F, 0.5f * (xl + xh), 0.5f * (yl + yh),
+                                0.5f * (xh - xl), 0.5f * (yh - yl)))
+                m &= ~(1u << u);
+        }
+    }
+    return m;
+}
+// thread t < 16 of the block writes extent t of the bin's 8x8 blocks (face_block_mask's table)
+__device__ __forceinline__ void block_extents(float* ext, int t, int bx0, int by0, int S) {
+    if (t < 16) {
+        const int base = (t & 8) ? by0 : bx0, j = t & 3;
+        ext[t] = pix_center(base + 8 * j + ((t & 4) ? 7 : 0), S);
+    }
+}
+
+// stage staged-face slot `slot` of candidate face f (coordinates c) and its block mask.  HALF (the
+// 1024-thread variant, twice as many threads as staged faces): thread `slot` evaluates the mask's
+// block rows 0-1 and thread FST + slot rows 2-3 (stage_mask_rows), each writing its byte, so the edge
+// culls of a round spread over every wave of the block.
+template <int FST, bool CULL, bool HALF>
+__device__ __forceinline__ void stage_face(float4* s_face, uint16_t* s_bm, int slot, const float* __restrict__ c, int f,
+                                           const float* __restrict__ ext) {
+    float4* e = s_face + slot;
     const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
     const float x2 = c[6], y2 = c[7], z2 = c[8];
-    e[0 * FST] = make_float4(fminf(fminf(x0, x1), x2), fmaxf(fmaxf(x0, x1), x2), fminf(fminf(y0, y1), y2),
-                       fmaxf(fmaxf(y0, y1), y2));
+    const float xmin = fminf(fminf(x0, x1), x2), xmax = fmaxf(fmaxf(x0, x1), x2);
+    const float ymin = fminf(fminf(y0, y1), y2), ymax = fmaxf(fmaxf(y0, y1), y2);
+    e[0 * FST] = make_float4(xmin, xmax, ymin, ymax);
+    const uint32_t m = face_block_mask<CULL>(x0, y0, x1, y1, x2, y2, xmin, xmax, ymin, ymax, ext, 0, HALF ? 2 : 4);
+    if (HALF) reinterpret_cast<uint8_t*>(s_bm)[2 * slot] = (uint8_t)m;
+    else s_bm[slot] = (uint16_t)m;
     e[1 * FST] = make_float4(fminf(fminf(z0, z1), z2), x1 * y2 - x2 * y1, x0 * y1 - x1 * y0, x2 * y0 - x0 * y2);
     e[2 * FST] = make_float4(y0, y2, x0, x2);
     e[3 * FST] = make_float4(x1 - x0, x0 - x2, y1 - y0, y0 - y2);
@@ -508,6 +557,15 @@ __device__ __forceinline__ void stage_face(float4* e, const float* __restrict__ 
                     in_range(z0, 0x1p-20f, 0x1p20f) && in_range(z1, 0x1p-20f, 0x1p20f) &&
                     in_range(z2, 0x1p-20f, 0x1p20f);
     e[6 * FST] = make_float4(rcp_nr(z0), rcp_nr(z1), rcp_nr(z2), __int_as_float(ok ? 1 : 0));
+}
+template <bool CULL>
+__device__ __forceinline__ void stage_mask_rows(uint16_t* s_bm, int slot, const float* __restrict__ c,
+                                                const float* __restrict__ ext) {
+    const float x0 = c[0], y0 = c[1], x1 = c[3], y1 = c[4], x2 = c[6], y2 = c[7];
+    const float xmin = fminf(fminf(x0, x1), x2), xmax = fmaxf(fmaxf(x0, x1), x2);
+    const float ymin = fminf(fminf(y0, y1), y2), ymax = fmaxf(fmaxf(y0, y1), y2);
+    const uint32_t m = face_block_mask<CULL>(x0, y0, x1, y1, x2, y2, xmin, xmax, ymin, ymax, ext, 2, 2);
+    reinterpret_cast<uint8_t*>(s_bm)[2 * slot + 1] = (uint8_t)(m >> 8);
 }
 
 // per-wave phase timestamps of the fused forward (timing builds only, tools/fwd_timing.py)
@@ -537,7 +595,7 @@ constexpr int FWD_WPE = 8;
 // map is not read back and k_shade has no launch of its own.
 // CC (SHADE only): the channel count as a compile-time constant; CC = MAXC means rgb + sil + depth,
 // so the epilogue's draw-flag tests and per-channel guards fold away (0: sh.C / sh.draw at run time)
-template <int NTF, bool SHADE, int CC = 0, bool XCULL = false>
+template <int NTF, bool SHADE, int CC = 0>
 __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
@@ -548,14 +606,19 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
-    // deep bins: small faces over each 8x8 block (XCULL: the 256-thread variant too, for a split
-    // forward's shallow bins)
-    constexpr bool CULL = NTF == 1024 || XCULL;
+    // the edge cull of staged faces per 8x8 block (face_block_mask).  Once a cost of ~40 VALU per wave
+    // and 64 staged faces in every walk's ballot, which only the deep-bin variant paid back (headline
+    // +2-5 %); evaluated once per (face, overlapped block) at staging since v56, it pays in every
+    // variant (headline forward 0.1444 -> 0.1397 ms, torus 0.1207 -> 0.1181 ms, the car unchanged;
+    // same-box A/B, 3 runs each, gpurun_out/e3)
+    constexpr bool CULL = true;
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
     __shared__ int s_scan[C::NW];
     __shared__ int s_next;  // (dyn) next 8x8 block to walk
     float4* s_face = reinterpret_cast<float4*>(s_raw);
     int* s_cand = reinterpret_cast<int*>(s_raw + FCAP * FREC * 16);
+    uint16_t* s_bm = reinterpret_cast<uint16_t*>(s_raw + FCAP * FREC * 16 + CAND * 4);  // staged faces' block masks
+    float* s_ext = reinterpret_cast<float*>(s_raw + FCAP * FREC * 16 + CAND * 4 + FCAP * 2);  // block extents
 
     const int S = g.S;
     int b, bin_x, bin_y;
@@ -572,6 +635,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     const int by0 = bin_y * COARSE;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: block extents in SGPRs
+    block_extents(s_ext, t, bx0, by0, S);  // read after the first barrier below
 
     const uint32_t* words = mask + ((long long)b * g.nbins + bin) * g.nwords;
     const float* frb = face_records + (long long)b * F * rs;
@@ -630,7 +694,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 #endif
             if (t < ncand) {
                 const int f = s_cand[t];
-                stage_face<FCAP>(s_face + t, frb + f * rs, f);
+                stage_face<FCAP, CULL, false>(s_face, s_bm, t, frb + f * rs, f, s_ext);
             }
             __syncthreads();
 #ifdef NR_FWD_TIMING
@@ -647,8 +711,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                 // the block's pixel-centre extent: lanes 0 / 7 hold its first / last column, lanes
                 // 0 / 56 its first / last row (read into SGPRs, no recomputation)
                 const float xp = pix_center(bx0 + ox + (lane & 7), S), yp = pix_center(by0 + oy + (lane >> 3), S);
-                walk_block<FCAP, CULL, SHADE>(s_face, ncand, lane, xp, yp, lane_value(xp, 0), lane_value(xp, 7),
-                                              lane_value(yp, 0), lane_value(yp, 56), near, far, delta, depth_min, best);
+                walk_block<FCAP, SHADE>(s_face, s_bm, u, ncand, lane, xp, yp, near, far, delta, depth_min, best);
                 int id = best;
                 if (SHADE) {  // best is the staging slot: its face id is in the record's row 5
                     id = best >= 0 ? __float_as_int(s_face[5 * FCAP + best].w) : -1;
@@ -664,17 +727,14 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         float xp[NSUB], yp[NSUB];
         float depth_min[NSUB];
         int best[NSUB];
-        float xcl[NSUB], xch[NSUB], ycl[NSUB], ych[NSUB];
+        int ublk[NSUB];  // the 8x8 blocks' bits in the block masks
 #pragma unroll
         for (int k = 0; k < NSUB; k++) {
             int ox, oy;
             C::block_of(wid, k, ox, oy);
             xp[k] = pix_center_div(bx0 + ox + (lane & 7), S);
             yp[k] = pix_center_div(by0 + oy + (lane >> 3), S);
-            xcl[k] = lane_value(xp[k], 0);
-            xch[k] = lane_value(xp[k], 7);
-            ycl[k] = lane_value(yp[k], 0);
-            ych[k] = lane_value(yp[k], 56);
+            ublk[k] = (oy >> 3) * 4 + (ox >> 3);
             depth_min[k] = far;
             best[k] = -1;
         }
@@ -698,9 +758,12 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 #ifdef NR_FWD_TIMING
                     const unsigned long long ts0_ = clock64();
 #endif
+                    constexpr bool HALF = NTF >= 2 * FCAP;
                     if (t < n) {
                         const int f = s_cand[j0 + t];
-                        stage_face<FCAP>(s_face + t, frb + f * rs, f);
+                        stage_face<FCAP, CULL, HALF>(s_face, s_bm, t, frb + f * rs, f, s_ext);
+                    } else if (HALF && t >= FCAP && t - FCAP < n) {
+                        stage_mask_rows<CULL>(s_bm, t - FCAP, frb + s_cand[j0 + t - FCAP] * rs, s_ext);
                     }
                     __syncthreads();
 #ifdef NR_FWD_TIMING
@@ -709,13 +772,13 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                     if (CULL && total0 >= ZCULL_MIN) {  // (a separate instantiation: the plain walk's code unchanged)
 #pragma unroll
                         for (int k = 0; k < NSUB; k++)
-                            walk_block<FCAP, CULL, false, CULL>(s_face, n, lane, xp[k], yp[k], xcl[k], xch[k], ycl[k], ych[k],
-                                                                near, far, delta, depth_min[k], best[k]);
+                            walk_block<FCAP, false, true>(s_face, s_bm, ublk[k], n, lane, xp[k], yp[k], near, far, delta,
+                                                          depth_min[k], best[k]);
                     } else {
 #pragma unroll
                         for (int k = 0; k < NSUB; k++)
-                            walk_block<FCAP, CULL, false>(s_face, n, lane, xp[k], yp[k], xcl[k], xch[k], ycl[k], ych[k], near,
-                                                          far, delta, depth_min[k], best[k]);
+                            walk_block<FCAP, false>(s_face, s_bm, ublk[k], n, lane, xp[k], yp[k], near, far, delta,
+                                                    depth_min[k], best[k]);
                     }
                     __syncthreads();
                 }

@@ -240,17 +240,12 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 1);
             int e = check_launch("k_raster_fwd");
             if (e) return e;
-            // the 256-thread rest also culls its faces per 8x8 block by their edges (XCULL: the car's
-            // shallow bins hold slivers and large faces whose boxes cover blocks their edges miss; car
-            // forward 0.533-0.551 -> 0.508-0.509 ms, step 1.016-1.027 -> 0.968-0.989 ms, same-box A/B,
-            // 2 runs each, gpurun_out/e1)
-            constexpr bool XC = true;
             if (sh.C == MAXC)
-                hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC, XC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
+                hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
                                    bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
                                    split_cnt, 2);
             else
-                hipLaunchKernelGGL((k_raster_fwd<256, true, 0, XC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs, bbox,
+                hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs, bbox,
                                    mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 2);
             e = check_launch("k_raster_fwd");
             if (e) return e;

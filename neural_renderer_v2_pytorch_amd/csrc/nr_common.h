@@ -109,11 +109,14 @@ Geom make_geom(int F, int S) {
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-// workspace layout: [bbox int2 B*F][mask u32 B*nbins*nwords][bin candidate counts i32 B*nbins]
-// [bin order i32 B*nbins] (the last two: deep-bin dispatch order, run_face_index)
+// workspace layout: [bbox int2 B*F][mask u32 B*nbins*nwords][per-face-group bin candidate counts u8
+// B*groups*nbins][bin order i32 B*nbins][split counts] (the last three: deep-bin dispatch order,
+// run_face_index; groups = the setup's face groups of SETUP_FACES)
 size_t ws_bbox_bytes(int B, int F) { return align_up((size_t)B * F * sizeof(int2)); }
 size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins * g.nwords * 4); }
-size_t ws_order_bytes(int B, const Geom& g) { return 2 * align_up((size_t)B * g.nbins * 4) + 256; }  // + the split counts
+inline int setup_groups(const Geom& g) { return (g.nwords + SETUP_FACES / 32 - 1) / (SETUP_FACES / 32); }
+size_t ws_part_bytes(int B, const Geom& g) { return align_up((size_t)B * setup_groups(g) * g.nbins); }
+size_t ws_order_bytes(int B, const Geom& g) { return ws_part_bytes(B, g) + align_up((size_t)B * g.nbins * 4) + 256; }
 
 // ------------------------------------------------------------------------------------------------
 // device helpers

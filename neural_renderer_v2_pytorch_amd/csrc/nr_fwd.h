@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     const float* __restrict__ vt, long long vt_bstride, int Vt,
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
                                                     int uv_items, float* __restrict__ fnorm, TexPack pk, ZeroFill zf,
-                                                    int* __restrict__ bin_count, int xcd_items) {
+                                                    uint8_t* __restrict__ bin_part, int xcd_items) {
     __shared__ int2 s_bb[SETUP_FACES];
     // the block's face records, assembled per face and then written out coalesced (a record per lane
     // would store 64-B strided rows); the bin-mask words reuse the space afterwards
@@ -158,12 +158,17 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
             const int bin = p / nw, wi = p % nw;
             mask[((long long)b * nbins + bin) * nwords + w0 + wi] = s_mask[bin * (SETUP_FACES / 32) + wi];
         }
-        if (bin_count) {  // candidate faces per bin (zeroed before the launch), for the deep-first order
+        if (bin_part) {
+            // this face group's candidate faces per bin (at most SETUP_FACES: a byte), a row of
+            // [B, groups, nbins] that k_bin_order sums over the groups for the deep-first order: every
+            // entry is written, so the counts need no zero fill (a memset launch per forward until v56)
+            // and no atomics
+            uint8_t* row = bin_part + ((long long)b * gridDim.x + grp) * nbins;
             for (int bin = t; bin < nbins; bin += blockDim.x) {
                 int pc = 0;
 #pragma unroll
                 for (int wi = 0; wi < SETUP_FACES / 32; wi++) pc += __builtin_popcount(s_mask[bin * (SETUP_FACES / 32) + wi]);
-                if (pc) atomicAdd(&bin_count[(long long)b * nbins + bin], pc);
+                row[bin] = (uint8_t)pc;
             }
         }
         zero_fill(zf);
@@ -228,10 +233,12 @@ constexpr int ORDER_MAX_ENTRIES = 64 * 256;
 // (ORDER_EMPTY, the entry flag of a bin without candidates, is in nr_common.h with ordered_bin)
 // split (optional): per list, the length of its prefix of bins with >= 2^(split_bucket - 1) candidate
 // faces, at most cap (the deep launch of a split forward, run_face_index)
-__global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt, int* __restrict__ order, int B,
-                                                    int nbins, int* __restrict__ split, int split_bucket, int cap) {
+// parts: the setup's per-(item, face group, bin) candidate counts [B, groups, nbins] (k_face_setup)
+__global__ __launch_bounds__(1024) void k_bin_order(const uint8_t* __restrict__ parts, int groups, int* __restrict__ order,
+                                                    int B, int nbins, int* __restrict__ split, int split_bucket, int cap) {
     __shared__ int s_h[ORDER_MAX_ENTRIES / 64][ORDER_BUCKETS];
     __shared__ int s_base[ORDER_BUCKETS];
+    __shared__ uint8_t s_bk[ORDER_MAX_ENTRIES];  // each entry's count bucket
     const bool per_xcd = gridDim.x == 8;
     const int x = blockIdx.x;
     const int items = per_xcd ? B / 8 : B;
@@ -244,9 +251,40 @@ __global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt,
         const int j = k / nbins;
         return (per_xcd ? x + 8 * j : j) * nbins + (k - j * nbins);
     };
+    // each entry's candidate count, the face groups' counts summed, as its bucket: four consecutive
+    // bins of an item per thread and 32-bit loads when the bins come in fours (a multiple of 4 per item)
+    if (nbins % 4 == 0) {
+        for (int q = threadIdx.x; q < n / 4; q += blockDim.x) {
+            const int k = 4 * q, e = entry(k), b = e / nbins, bin = e - b * nbins;
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(parts + (long long)b * groups * nbins + bin);
+            int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll 8
+            for (int gr = 0; gr < groups; gr++) {
+                const uint32_t v = p[(long long)gr * (nbins / 4)];
+                c0 += v & 0xffu;
+                c1 += (v >> 8) & 0xffu;
+                c2 += (v >> 16) & 0xffu;
+                c3 += v >> 24;
+            }
+            s_bk[k] = (uint8_t)count_bucket(c0);
+            s_bk[k + 1] = (uint8_t)count_bucket(c1);
+            s_bk[k + 2] = (uint8_t)count_bucket(c2);
+            s_bk[k + 3] = (uint8_t)count_bucket(c3);
+        }
+    } else {
+        for (int k = threadIdx.x; k < n; k += blockDim.x) {
+            const int e = entry(k), b = e / nbins, bin = e - b * nbins;
+            const uint8_t* p = parts + (long long)b * groups * nbins + bin;
+            int c = 0;
+#pragma unroll 8
+            for (int gr = 0; gr < groups; gr++) c += p[(long long)gr * nbins];
+            s_bk[k] = (uint8_t)count_bucket(c);
+        }
+    }
+    __syncthreads();
     for (int ch = wid; ch < nch; ch += nw) {
         const int k = ch * 64 + lane;
-        const int bk = k < n ? count_bucket(cnt[entry(k)]) : -1;
+        const int bk = k < n ? (int)s_bk[k] : -1;
 #pragma unroll
         for (int b = 0; b < ORDER_BUCKETS; b++) {
             const int c = __popcll(__ballot(bk == b));
@@ -274,7 +312,7 @@ __global__ __launch_bounds__(1024) void k_bin_order(const int* __restrict__ cnt,
     for (int ch = wid; ch < nch; ch += nw) {
         const int k = ch * 64 + lane;
         const int e = k < n ? entry(k) : 0;
-        const int bk = k < n ? count_bucket(cnt[e]) : -1;
+        const int bk = k < n ? (int)s_bk[k] : -1;
         int rank = 0;
 #pragma unroll
         for (int b = 0; b < ORDER_BUCKETS; b++) {
@@ -532,21 +570,21 @@ __device__ __forceinline__ void block_extents(float* ext, int t, int bx0, int by
     }
 }
 
-// stage staged-face slot `slot` of candidate face f (coordinates c) and its block mask.  HALF (the
-// 1024-thread variant, twice as many threads as staged faces): thread `slot` evaluates the mask's
+// stage staged-face slot `slot` of candidate face f (coordinates c) and its block mask.  half (the
+// 1024-thread variant: twice as many threads as staged faces): thread `slot` evaluates the mask's
 // block rows 0-1 and thread FST + slot rows 2-3 (stage_mask_rows), each writing its byte, so the edge
 // culls of a round spread over every wave of the block.
-template <int FST, bool CULL, bool HALF>
+template <int FST, bool CULL>
 __device__ __forceinline__ void stage_face(float4* s_face, uint16_t* s_bm, int slot, const float* __restrict__ c, int f,
-                                           const float* __restrict__ ext) {
+                                           const float* __restrict__ ext, bool half) {
     float4* e = s_face + slot;
     const float x0 = c[0], y0 = c[1], z0 = c[2], x1 = c[3], y1 = c[4], z1 = c[5];
     const float x2 = c[6], y2 = c[7], z2 = c[8];
     const float xmin = fminf(fminf(x0, x1), x2), xmax = fmaxf(fmaxf(x0, x1), x2);
     const float ymin = fminf(fminf(y0, y1), y2), ymax = fmaxf(fmaxf(y0, y1), y2);
     e[0 * FST] = make_float4(xmin, xmax, ymin, ymax);
-    const uint32_t m = face_block_mask<CULL>(x0, y0, x1, y1, x2, y2, xmin, xmax, ymin, ymax, ext, 0, HALF ? 2 : 4);
-    if (HALF) reinterpret_cast<uint8_t*>(s_bm)[2 * slot] = (uint8_t)m;
+    const uint32_t m = face_block_mask<CULL>(x0, y0, x1, y1, x2, y2, xmin, xmax, ymin, ymax, ext, 0, half ? 2 : 4);
+    if (half) reinterpret_cast<uint8_t*>(s_bm)[2 * slot] = (uint8_t)m;
     else s_bm[slot] = (uint16_t)m;
     e[1 * FST] = make_float4(fminf(fminf(z0, z1), z2), x1 * y2 - x2 * y1, x0 * y1 - x1 * y0, x2 * y0 - x0 * y2);
     e[2 * FST] = make_float4(y0, y2, x0, x2);
@@ -589,6 +627,7 @@ __device__ unsigned long long g_fwd_t[NR_FTIMING_MAX];
 #endif
 
 // 8 waves/SIMD (at v37 7 waves, with no spilled register, measured the same)
+// (the 256-thread variant at 7 waves/SIMD: car forward +10 %, gpurun_out/e6)
 constexpr int FWD_WPE = 8;
 // SHADE (NTF == 256, anti-aliasing, no lights / backgrounds): the block also shades its bin's 16x16
 // output pixels (k_shade's work, shade_quad) from the face ids it has just found, so the face-index
@@ -692,9 +731,11 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 #ifdef NR_FWD_TIMING
             const unsigned long long ts0_ = clock64();
 #endif
+            // (one thread per face: splitting the masks of rounds of at most 128 faces over the idle
+            // threads measured the same, and spilled a register, gpurun_out/e6)
             if (t < ncand) {
                 const int f = s_cand[t];
-                stage_face<FCAP, CULL, false>(s_face, s_bm, t, frb + f * rs, f, s_ext);
+                stage_face<FCAP, CULL>(s_face, s_bm, t, frb + f * rs, f, s_ext, false);
             }
             __syncthreads();
 #ifdef NR_FWD_TIMING
@@ -758,12 +799,12 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 #ifdef NR_FWD_TIMING
                     const unsigned long long ts0_ = clock64();
 #endif
-                    constexpr bool HALF = NTF >= 2 * FCAP;
+                    constexpr bool half = NTF >= 2 * FCAP;  // the 1024-thread variant
                     if (t < n) {
                         const int f = s_cand[j0 + t];
-                        stage_face<FCAP, CULL, HALF>(s_face, s_bm, t, frb + f * rs, f, s_ext);
-                    } else if (HALF && t >= FCAP && t - FCAP < n) {
-                        stage_mask_rows<CULL>(s_bm, t - FCAP, frb + s_cand[j0 + t - FCAP] * rs, s_ext);
+                        stage_face<FCAP, CULL>(s_face, s_bm, t, frb + f * rs, f, s_ext, half);
+                    } else if (half && t >= NTF / 2 && t - NTF / 2 < n) {
+                        stage_mask_rows<CULL>(s_bm, t - NTF / 2, frb + s_cand[j0 + t - NTF / 2] * rs, s_ext);
                     }
                     __syncthreads();
 #ifdef NR_FWD_TIMING

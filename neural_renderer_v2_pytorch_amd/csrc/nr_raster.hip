@@ -140,8 +140,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     g.B = B;
     int2* bbox = (int2*)ws;
     uint32_t* mask = (uint32_t*)((char*)ws + ws_bbox_bytes(B, F));
-    int* bin_count = (int*)((char*)mask + ws_mask_bytes(B, g));
-    int* bin_order = (int*)((char*)bin_count + ws_order_bytes(B, g) / 2);
+    uint8_t* bin_part = (uint8_t*)mask + ws_mask_bytes(B, g);
+    int* bin_order = (int*)(bin_part + ws_part_bytes(B, g));
     if (B == 0) return NR_OK;
     // forward block size (k_raster_fwd notes): 256 threads when the grid alone fills the chip many
     // times over and the bins are shallow; 1024 when it does not, or when the bins are deep (F per bin
@@ -154,8 +154,6 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     const long long order_list = (B % 8 == 0 ? B / 8 : B) * (long long)g.nbins;  // entries per k_bin_order block
     const bool ordered = F > 0 && ntf == 1024 && faces_per_bin >= 24.0 &&
                          (long long)g.nbins * (SETUP_FACES / 32) <= SETUP_LDS_WORDS && order_list <= ORDER_MAX_ENTRIES;
-    if (ordered && hipMemsetAsync(bin_count, 0, (size_t)B * g.nbins * 4, st) != hipSuccess)
-        return check_launch("hipMemsetAsync");
     // the setup's idle threads repack the textures when that takes them up to 32 texels each; with no
     // setup launch, or a texture too large for that, the repacking gets a launch of its own
     const long long setup_idle = (long long)((F + SETUP_FACES - 1) / SETUP_FACES) * B * (256 - SETUP_FACES);
@@ -182,11 +180,11 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
                                rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk, zf,
-                               ordered ? bin_count : nullptr, B % 8 == 0);
+                               ordered ? bin_part : nullptr, B % 8 == 0);
         else
             hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
-                               nullptr, pk, zf, ordered ? bin_count : nullptr, B % 8 == 0);
+                               nullptr, pk, zf, ordered ? bin_part : nullptr, B % 8 == 0);
         int e = check_launch("k_face_setup");
         if (e) return e;
         if (lit && V > 0) {
@@ -214,8 +212,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     if (ordered && fuse && B % 8 == 0 && Bcap <= B) side = side_stream(st);
 #endif
     if (ordered) {
-        hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_count, bin_order, B, g.nbins,
-                           side ? split_cnt : nullptr, SPLIT_BUCKET, Bcap / 8 * g.nbins);
+        hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,
+                           g.nbins, side ? split_cnt : nullptr, SPLIT_BUCKET, Bcap / 8 * g.nbins);
         const int e = check_launch("k_bin_order");
         if (e) return e;
     }

@@ -211,9 +211,14 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
 #ifndef NR_NO_SPLIT
     if (ordered && fuse && B % 8 == 0 && Bcap <= B) side = side_stream(st);
 #endif
+#ifdef NR_DEEP_CAP
+    const int deep_cap = min(NR_DEEP_CAP, Bcap / 8 * g.nbins);
+#else
+    const int deep_cap = Bcap / 8 * g.nbins;
+#endif
     if (ordered) {
         hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,
-                           g.nbins, side ? split_cnt : nullptr, SPLIT_BUCKET, Bcap / 8 * g.nbins);
+                           g.nbins, side ? split_cnt : nullptr, SPLIT_BUCKET, deep_cap);
         const int e = check_launch("k_bin_order");
         if (e) return e;
     }

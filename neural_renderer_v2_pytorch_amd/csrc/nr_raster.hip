@@ -131,6 +131,20 @@ SideStream* side_stream(hipStream_t st) {
     return &x;
 }
 
+// 1024-thread blocks of k_raster_fwd resident at once on one XCD of the current device: two per CU
+// (32 waves and 2 x 62.6 KB of LDS), the CUs dealt evenly over the 8 XCDs
+static int deep_slots_per_xcd() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 64;
+    if (!cached[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        __atomic_store_n(&cached[dev], 2 * max(cus / 8, 1), __ATOMIC_RELAXED);
+    }
+    return __atomic_load_n(&cached[dev], __ATOMIC_RELAXED);
+}
+
 static int run_face_index(const float* vertices, const int32_t* faces_idx, float* face_records, int32_t* fim,
                           int B, int V, int F, int S, float near, float far, int draw_backside, float delta,
                           void* ws, size_t ws_bytes, hipStream_t st, const NrRasterArgs* ra, float* images,
@@ -211,11 +225,14 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
 #ifndef NR_NO_SPLIT
     if (ordered && fuse && B % 8 == 0 && Bcap <= B) side = side_stream(st);
 #endif
-#ifdef NR_DEEP_CAP
-    const int deep_cap = min(NR_DEEP_CAP, Bcap / 8 * g.nbins);
-#else
-    const int deep_cap = Bcap / 8 * g.nbins;
-#endif
+    // the deep launch takes at most 7/8 of one XCD's slots for 1024-thread blocks per list (two per CU,
+    // by their waves and LDS), so every deep bin is dispatched at once: a deep block waiting for a slot
+    // starves behind the rest launch's 256-thread blocks, which take every CU space that frees up (at
+    // 75 deep bins per list the last ones started at 430 us of a 535 us car forward,
+    // profiles/r05_v56_car_fwd_wave_phases.txt); the bins past the cap go to the rest launch.  Car
+    // forward 0.49-0.50 -> 0.44 ms at 56 per list (48: the same; 40: 0.57 ms; 64 or no cap: 0.50 ms;
+    // same-box A/B, 3 runs each, gpurun_out/e7)
+    const int deep_cap = min(Bcap / 8 * g.nbins, deep_slots_per_xcd() * 7 / 8);
     if (ordered) {
         hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,
                            g.nbins, side ? split_cnt : nullptr, SPLIT_BUCKET, deep_cap);
@@ -239,7 +256,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             // for the side stream's launch
             if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
                 return check_launch("hipEventRecord");
-            hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, Bcap), dim3(1024), 0, st, face_records, rs, bbox,
+            // (a grid of exactly the cap's blocks: every block past a list's deep prefix exits at once, but
+            // each still needs a 1024-thread slot to be dispatched in)
+            hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(8 * deep_cap), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 1);
             int e = check_launch("k_raster_fwd");
             if (e) return e;

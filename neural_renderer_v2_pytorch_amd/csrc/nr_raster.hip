@@ -230,8 +230,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     // starves behind the rest launch's 256-thread blocks, which take every CU space that frees up (at
     // 75 deep bins per list the last ones started at 430 us of a 535 us car forward,
     // profiles/r05_v56_car_fwd_wave_phases.txt); the bins past the cap go to the rest launch.  Car
-    // forward 0.49-0.50 -> 0.44 ms at 56 per list (48: the same; 40: 0.57 ms; 64 or no cap: 0.50 ms;
-    // same-box A/B, 3 runs each, gpurun_out/e7)
+    // forward 0.49-0.50 -> 0.44 ms at 56 per list (48: the same; 40: 0.57 ms, the bins it leaves to the
+    // 256-thread launch then end last; 64: 0.46-0.48 ms; no cap: 0.50 ms; same-box A/Bs, 3 runs each,
+    // gpurun_out/e7, e9)
     const int deep_cap = min(Bcap / 8 * g.nbins, deep_slots_per_xcd() * 7 / 8);
     if (ordered) {
         hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,

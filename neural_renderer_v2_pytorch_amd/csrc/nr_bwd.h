@@ -217,9 +217,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     Shade sh = sh_in;
     if (!LIT) sh.nl = 0;
     if (!BG) sh.bg = nullptr;
-    if (CC == MAXC) {
-        // the only 5-channel render; launched only with anti-aliasing and a power-of-two raster
-        sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;
+    if (CC) {
+        // CC = MAXC: rgb + sil + depth (the only 5-channel render); CC = 4: rgb + sil (rasterize_rgba,
+        // Renderer.render); launched only with anti-aliasing and a power-of-two raster
+        sh.draw = static_draw(CC);
         a.aa = 1;
         a.step_pow2 = 1;
     }
@@ -836,6 +837,9 @@ void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, con
         g_last_bwd.store(LaunchRec{2 * NT, 0});
     } else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2) {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC>), grid, dim3(NT), 0, st, ba, g, sh);
+        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE});
+    } else if (FEAT == 0 && sh.draw == static_draw(4) && ba.aa && ba.step_pow2) {
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, 4>), grid, dim3(NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE});
     } else {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);

@@ -23,6 +23,11 @@ inline int setup_lds_words(int nbins) {
     return (m <= SETUP_LDS_WORDS && m > stage) ? m : stage;
 }
 constexpr int MAXC = 5;            // max output channels
+// the draw flags of a compile-time channel count (the instantiations with static channels): 5 = rgb +
+// silhouettes + depth, 4 = rgb + silhouettes (rgba)
+__host__ __device__ constexpr int static_draw(int cc) {
+    return cc == 5 ? (NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH) : (NR_DRAW_RGB | NR_DRAW_SILHOUETTES);
+}
 
 thread_local std::string g_err;
 

@@ -632,8 +632,9 @@ constexpr int FWD_WPE = 8;
 // SHADE (NTF == 256, anti-aliasing, no lights / backgrounds): the block also shades its bin's 16x16
 // output pixels (k_shade's work, shade_quad) from the face ids it has just found, so the face-index
 // map is not read back and k_shade has no launch of its own.
-// CC (SHADE only): the channel count as a compile-time constant; CC = MAXC means rgb + sil + depth,
-// so the epilogue's draw-flag tests and per-channel guards fold away (0: sh.C / sh.draw at run time)
+// CC (SHADE only): the channel count as a compile-time constant; CC = MAXC means rgb + sil + depth, 4
+// rgb + sil (static_draw), so the epilogue's draw-flag tests and per-channel guards fold away (0: sh.C /
+// sh.draw at run time)
 template <int NTF, bool SHADE, int CC = 0>
 __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
@@ -865,9 +866,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         // no backgrounds in this variant), as is every halo value.  With the bin flags the halo values
         // are not written: the backward reads a halo pixel of a flagged-empty bin as 0
         Shade sh = sh_in;
-        if (CC == MAXC) {
-            sh.C = MAXC;
-            sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;
+        if (CC) {
+            sh.C = CC;
+            sh.draw = static_draw(CC);
         }
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
@@ -884,9 +885,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         Shade sh = sh_in;
         sh.nl = 0;
         sh.bg = nullptr;
-        if (CC == MAXC) {
-            sh.C = MAXC;
-            sh.draw = NR_DRAW_RGB | NR_DRAW_SILHOUETTES | NR_DRAW_DEPTH;
+        if (CC) {
+            sh.C = CC;
+            sh.draw = static_draw(CC);
         }
         __syncthreads();
         NR_FTSTAMP(4, clock64());

@@ -250,7 +250,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         ProfScope _p(P_RASTER, st);
         const int rs = vertices ? FACE_REC : 9;
         g_last_fwd.store(LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
-                                        (fuse && ntf == 256 && sh.C == MAXC ? NR_LAUNCH_STATIC_CHANNELS : 0) |
+                                        (fuse && ntf == 256 && (sh.C == MAXC || sh.draw == static_draw(4)) ? NR_LAUNCH_STATIC_CHANNELS : 0) |
                                         (ordered ? NR_LAUNCH_DEEP_FIRST : 0) | (side ? NR_LAUNCH_SPLIT : 0)});
         if (side) {
             // fork: the side stream waits for the setup and the order; join: the caller's stream waits
@@ -267,6 +267,10 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                 hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
                                    bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
                                    split_cnt, 2);
+            else if (sh.draw == static_draw(4))  // rgba (the car): compile-time channels
+                hipLaunchKernelGGL((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
+                                   bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
+                                   split_cnt, 2);
             else
                 hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs, bbox,
                                    mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 2);
@@ -279,6 +283,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
             hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
+        else if (fuse && sh.draw == static_draw(4))  // rgba: compile-time channels
+            hipLaunchKernelGGL((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse)
             hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,

@@ -140,6 +140,7 @@ def car64(dev, oracle_mod):
     img.backward(g.to(dev))
     assert torch.isfinite(pv.grad).all() and torch.isfinite(leaf.grad).all()
     torch.cuda.synchronize()
+    bwd_launch = _lib.last_launch("k_raster_bwd")
     cache = {}
 
     def quarter(q):
@@ -149,7 +150,7 @@ def car64(dev, oracle_mod):
                                                      draw_depth=False))
         return cache[q]
     return dict(proj=proj, f=f, img=img.detach().cpu(), fim=fim.cpu().numpy(), gv=pv.grad.cpu(),
-                gt=leaf.grad.cpu(), launch=launch, quarter=quarter)
+                gt=leaf.grad.cpu(), launch=launch, bwd_launch=bwd_launch, quarter=quarter)
 
 
 @pytest.mark.parametrize("q", [0, 1, 2, 3])
@@ -159,6 +160,8 @@ def test_cfg3_car_subdivided_vs_oracle(car64, q):
     forward (1024-thread deep prefix, deepest bin first; asserted from the library's launch
     record); they hold more than one 512-face staging round."""
     assert car64["launch"] == (1024, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_DEEP_FIRST | _lib.NR_LAUNCH_SPLIT)
+    # rgba (rgb + silhouettes): the backward's compile-time 4-channel instantiation
+    assert car64["bwd_launch"] == (256, _lib.NR_LAUNCH_STATIC_CHANNELS | _lib.NR_LAUNCH_TWO_PX_PER_LANE)
     if q == 0:
         counts = _bin_candidates(car64["proj"][:4], car64["f"], 512)
         assert counts.max() > 512, counts.max()

@@ -812,7 +812,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             const float v = gsel * wsel;
             // the texel index as sample_texture clamps it (a clamped corner has weight 0)
             const int idx = min(max(direct_base(__float_as_int(rb.w)) + col + row * sh.tv.W, 0), HW - 1);
+#ifdef NR_ABL_NODIRECT  // timing builds only: no direct-sample atomics
+            if (slot >= 0 && ch < 3 && v == 12345.f) unsafeAtomicAdd(gtb + idx * 4 + ch, v);
+#else
             if (slot >= 0 && ch < 3 && v != 0.f) unsafeAtomicAdd(gtb + idx * 4 + ch, v);
+#endif
         }
     }
     NR_TSTAMP(6);

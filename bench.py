@@ -362,6 +362,7 @@ def pmc_passes(args, timeout_s=240):
     import pmc_traffic
     d = tempfile.mkdtemp(prefix="nr_pmc_")
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    # (the child runs warmup + steps = 4 steps: summarize's per-step traffic divides by that)
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--steps", "3", "--warmup", "1",
              "--batch", str(args.batch), "--image-size", str(args.image_size), "--level", str(args.level),
              "--mode", args.mode]
@@ -379,7 +380,7 @@ def pmc_passes(args, timeout_s=240):
                 return None, "pmc pass %d (%s) timed out" % (i, " ".join(counters))
             if p.returncode != 0:
                 return None, "pmc pass %d exited %d: %s" % (i, p.returncode, err.decode(errors="replace")[-300:])
-        return pmc_traffic.summarize(d, [args.batch, args.image_size, args.level, args.mode], verbose=False), \
+        return pmc_traffic.summarize(d, [args.batch, args.image_size, args.level, args.mode], verbose=False, steps=4), \
             "rocprofv3 --pmc, 3 passes in this run over 3 steps each; FETCH_SIZE/WRITE_SIZE calibrated on a 1 GiB stream"
     except Exception as e:  # a profiler failure must not lose the bench line
         return None, "pmc passes failed: %r" % (e,)
@@ -531,7 +532,8 @@ def main():
             pmc, pmc_note = pmc_passes(args)
     traffic = valu_busy = valu_insts = wait_share = None
     if pmc is not None:
-        traffic = pmc.get("hbm_bytes_per_launch", {}).get(dominant)
+        # per step (every launch of the kernel in a step; one for k_raster_bwd), like the algorithmic bytes
+        traffic = pmc.get("hbm_bytes_per_step", pmc.get("hbm_bytes_per_launch", {})).get(dominant)
         valu_busy = pmc.get("valu_busy", {}).get(dominant)
         valu_insts = pmc.get("valu_insts", {}).get(dominant)
         wait_share = pmc.get("wait_any_share", {}).get(dominant)
@@ -582,7 +584,8 @@ def main():
                      # otherwise latency
                      "limiter": limiter},
         "pmc_all_kernels": None if pmc is None else {
-            k: {"traffic": pmc["hbm_bytes_per_launch"].get(k), "valu_busy": round(pmc.get("valu_busy", {}).get(k, 0.0), 4),
+            k: {"traffic": pmc.get("hbm_bytes_per_step", pmc["hbm_bytes_per_launch"]).get(k),
+                "valu_busy": round(pmc.get("valu_busy", {}).get(k, 0.0), 4),
                 "wait_share": round(pmc.get("wait_any_share", {}).get(k, 0.0), 4)} for k in pmc["hbm_bytes_per_launch"]},
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "step_roofline_frac": round(total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),

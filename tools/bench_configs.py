@@ -296,7 +296,8 @@ def pmc_traffic(name, timeout_s=240):
                    "--", sys.executable, os.path.abspath(__file__), "--pmc-child", name]
             subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout_s, check=True,
                            cwd=ROOT, env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
-        return pt.summarize(d, [name], verbose=False)["hbm_bytes_per_launch"]
+        # pmc_child runs steps + 1 = 4 steps: per-step bytes (a split forward launches k_raster_fwd twice)
+        return pt.summarize(d, [name], verbose=False, steps=4)["hbm_bytes_per_step"]
     finally:
         shutil.rmtree(d, ignore_errors=True)
 

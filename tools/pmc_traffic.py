@@ -41,8 +41,10 @@ def load(d, counter):
 SIMDS, XCDS, VALU_CYCLES = 1024, 8, 2  # MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU op issues over 2 cycles
 
 
-def summarize(d, config=None, verbose=True):
-    """Per-kernel HBM bytes, VALU instruction counts and shares from the passes under d/p1..p3."""
+def summarize(d, config=None, verbose=True, steps=None):
+    """Per-kernel HBM bytes, VALU instruction counts and shares from the passes under d/p1..p3.  With
+    `steps` (the fwd+bwd steps the profiled child ran), also each kernel's bytes per step: the sum
+    over its launches / steps (a split forward launches k_raster_fwd twice per step)."""
     fetch, write = load(os.path.join(d, "p1"), "FETCH_SIZE"), load(os.path.join(d, "p2"), "WRITE_SIZE")
     p3 = os.path.join(d, "p3")
     valu, grbm = load(p3, "SQ_INSTS_VALU"), load(p3, "GRBM_GUI_ACTIVE")
@@ -64,6 +66,12 @@ def summarize(d, config=None, verbose=True):
         out["read_bytes"][k] = f * rscale
         out["write_bytes"][k] = w * wscale
         out["hbm_bytes_per_launch"][k] = int(f * rscale + w * wscale)
+        if steps:
+            # launches per step rounded (a set-up launch outside the steps, e.g. cfg5's target render, is
+            # one extra launch, not a second per step), at least one
+            lps = max(1, round(max(len(fetch[k]), len(write[k])) / steps))
+            out.setdefault("hbm_bytes_per_step", {})[k] = int((f * rscale + w * wscale) * lps)
+            out.setdefault("launches_per_step", {})[k] = lps
         if valu.get(k) and grbm.get(k):
             mean = lambda v: sum(v) / len(v)  # noqa: E731
             # VALU issue share: wave-instructions x 2 cycles over the SIMD-cycles of the launch

@@ -388,6 +388,44 @@ def test_split_forward_capped_vs_oracle(oracle_mod, dev):
     assert torch.equal(fim8, fim[:8]) and torch.equal(img8, img[:8])
 
 
+def test_split_forward_from_exiting_threads(dev):
+    """The split forward's side stream is per host thread and released when the thread ends
+    (nr_raster.hip SideStreamTable): split forwards rendered from three worker threads that start,
+    render and exit one after another, then again from this thread, all give the same images and
+    face-index maps (the streams and events of the ended threads are destroyed, not reused)."""
+    import threading
+    r = np.random.RandomState(12)
+    S, F, B = 64, 4000, 16
+    cx = r.uniform(-0.9, 0.9, size=(B, F, 1))
+    cy = r.uniform(-0.9, 0.9, size=(B, F, 1))
+    x = (cx + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    y = (cy + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    z = r.uniform(0.5, 5.0, size=(B, F, 3)).astype(np.float32)
+    verts = torch.as_tensor(np.stack([x, y, z], -1).reshape(B, F * 3, 3), device=dev)
+    faces = torch.arange(F * 3, dtype=torch.int32, device=dev).reshape(F, 3)
+
+    def render():
+        hp = nr.RasterizeHyperparam(image_size=S // 2, anti_aliasing=True)
+        hp.draw_rgb = False
+        img, fim = nrr.rasterize_core(verts, faces, nr.RasterizeParam(), hp, return_face_index=True)
+        flags = _lib.last_launch("k_raster_fwd")[1]
+        torch.cuda.synchronize()
+        return img.cpu(), fim.cpu(), flags
+
+    want = render()
+    assert want[2] & _lib.NR_LAUNCH_SPLIT
+    got = []
+    for _ in range(3):
+        th = threading.Thread(target=lambda: got.append(render()))
+        th.start()
+        th.join()
+    got.append(render())
+    assert len(got) == 4
+    for img, fim, flags in got:
+        assert flags & _lib.NR_LAUNCH_SPLIT
+        assert torch.equal(img, want[0]) and torch.equal(fim, want[1])
+
+
 def test_headline_properties(dev):
     """Full headline config (B=64, 256^2 AA, ico 5120, rgb+sil+depth): size-independent properties."""
     B = 64

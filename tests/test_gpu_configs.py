@@ -10,7 +10,8 @@ checked against the CPU oracle on the GPU (through the C ABI, one batched call e
   cfg5  torus 250x100 (50000 faces) at 512^2 (1024^2 internal) through Renderer.render_silhouettes:
         face-index map bit-exact against the brute-force oracle (the 1024-thread forward's
         multi-word bin masks, nwords = 1563 > 1024), silhouette gradients; and the 200-step
-        example2-style Adam loop.
+        example2-style Adam loop, whose first 8 steps are also run through the oracle's CPU
+        pipeline and compared step by step (losses, vertex trajectory).
   k_raster_fwd<256>, two branches the headline never takes:
         * bins with more candidates than one 160-face staging round (the static-quadrant walk
           with per-pixel state carried across rounds, and the fused shading through s_fim): a
@@ -248,6 +249,58 @@ def test_cfg5_torus_adam_loop(dev):
     assert all(math.isfinite(x) for x in losses)
     # measured on an MI355X: 11610 -> 16.9 (step 100) -> 4.1 (step 200)
     assert losses[0] > 5000 and losses[-1] < 0.01 * losses[0], (losses[0], losses[-1])
+
+
+TRAJ_STEPS = 8
+# measured on an MI355X: the eight losses equal to the last bit; vertices apart by at most 8.9e-7
+# after 8 steps that moved them by up to 8.1e-3 (1.1e-4 of the move)
+TRAJ_LOSS_RTOL = 1e-5
+TRAJ_VERT_ATOL = 1e-3  # of the largest vertex move
+
+
+def test_cfg5_torus_adam_trajectory_vs_oracle(oracle_mod, dev):
+    """The first TRAJ_STEPS steps of cfg5's loop (example2.py:17-78: silhouette loss, Adam) run twice
+    from the same start: through the HIP rasterizer, and through the oracle's CPU pipeline
+    (oracle/oracle.py rasterize_core: the brute-force face-index scan and the torch-CPU stages).
+    Both legs share everything else -- the CPU camera composition, the target, the loss and a CPU
+    Adam -- so the two trajectories differ only by the rasterizer's rounding (its float atomics sum
+    in another order than the oracle's scatter), which Adam's per-coordinate normalisation can
+    amplify only for vertices whose gradient is near zero.  Pins the trajectory, not only the loss
+    drop of test_cfg5_torus_adam_loop."""
+    v, f = synthetic.torus(250, 100)
+    faces = torch.as_tensor(f, device=dev)
+    ren = _torus_renderer()
+    with torch.no_grad():
+        target = ren.render_silhouettes(torch.as_tensor(v[None] * 1.1, device=dev), faces).cpu()
+    legs = []
+    for use_gpu in (True, False):
+        verts = torch.nn.Parameter(torch.tensor(v[None]))  # a copy: Adam updates it in place
+        opt = torch.optim.Adam([verts], lr=0.001)
+        losses, path = [], []
+        for _ in range(TRAJ_STEPS):
+            opt.zero_grad()
+            proj = ren.transform_vertices(verts)  # CPU tensors: the reference's torch composition
+            if use_gpu:
+                hp = nr.RasterizeHyperparam(image_size=512)
+                hp.draw_rgb = hp.draw_depth = False
+                img = nrr.rasterize_silhouettes(proj.to(dev), faces, nr.RasterizeParam(), hp).cpu()
+            else:
+                img = oracle_mod.rasterize_core(proj, f, image_size=512, draw_rgb=False, draw_depth=False)[:, 0]
+            loss = ((img - target) ** 2).sum()
+            loss.backward()
+            opt.step()
+            losses.append(float(loss.detach()))
+            path.append(verts.detach().clone())
+        legs.append((np.array(losses), path))
+    (lg, pg), (lo, po) = legs
+    rel = np.abs(lg - lo) / np.abs(lo)
+    dv = [float((a - b).abs().max()) for a, b in zip(pg, po)]
+    moved = float((po[-1] - torch.as_tensor(v[None])).abs().max())
+    print("cfg5 trajectory: losses gpu %s oracle %s; max rel loss diff %.2e; max |dv| per step %s; "
+          "max vertex move %.3e" % (np.round(lg, 2), np.round(lo, 2), rel.max(), ["%.1e" % d for d in dv], moved))
+    assert lo[-1] < lo[0]
+    assert rel.max() <= TRAJ_LOSS_RTOL, rel
+    assert max(dv) <= TRAJ_VERT_ATOL * moved, (dv, moved)
 
 
 def test_fwd256_multi_round_bins_vs_oracle(oracle_mod, dev):

@@ -1,7 +1,7 @@
 """Per-wave phase timing of the forward k_raster_fwd on the headline workload (the fused <256, true>
 variant) or the car (--workload car: the split forward, its deep launch at 1024 threads and the rest
 at 256 on a side stream, each decoded with its own block size) (timing build, NR_FWD_TIMING).
-usage (GPU box): python tools/fwd_timing.py [--workload car] [extra -D flags...]
+usage (GPU box): python tools/fwd_timing.py [--workload car|cfg2] [extra -D flags...]
 Phases: mask words + candidate scan, face staging rounds (summed), candidate expansion + face walk,
 fim write + bin flag + LDS hand-over, shading epilogue; split by the bin's candidate count."""
 import ctypes
@@ -33,6 +33,11 @@ if WORKLOAD == "car":
     import bench_configs  # noqa: E402
     step, _, batch, size = bench_configs.cfg3_step(torch.device("cuda", 0))
     waves = 16  # deep bins: the 1024-thread variant
+elif WORKLOAD == "cfg2":  # the teapot, B = 4 (the 1024-thread variant: small batches)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs  # noqa: E402
+    step, meta = bench_configs.cfg2_step(torch.device("cuda", 0))
+    batch, size, waves = meta["batch"], meta["image_size"], 16
 else:
     args = bench.parse()
     w = bench.workload(args, 0, torch.device("cuda", 0))
@@ -50,6 +55,8 @@ nbins = (S // 32) ** 2
 HALF = (1 << 22) // 2  # NR_FTIMING_MAX / 2: a split forward's second launch stamps the upper half
 threads, flags = _lib.last_launch("k_raster_fwd")
 split = bool(flags & _lib.NR_LAUNCH_SPLIT)
+if not split:
+    waves = threads // 64
 buf = (ctypes.c_ulonglong * (2 * HALF))()
 assert L.nr_debug_fwd_timing(buf, ctypes.c_size_t(2 * HALF)) == 0
 raw = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)

@@ -37,8 +37,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "C
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    # defaults: steady state (five warm-up steps left the GPU short of it: 20 timed steps then took
+    # 0.380-0.385 ms each against 0.358-0.360 ms after 50, and 0.355 ms over 300; profiles/r05_warmup.txt)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--batch", type=int, default=64, help="items per GPU")
     p.add_argument("--image-size", type=int, default=256)
     p.add_argument("--level", type=int, default=4, help="ico-sphere subdivision level (4 -> 5120 faces)")

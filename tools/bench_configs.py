@@ -304,8 +304,9 @@ def pmc_traffic(name, timeout_s=240):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    # steady state (as bench.py: five warm-up steps left the GPU short of it, profiles/r05_warmup.txt)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=30)
     p.add_argument("--loop-steps", type=int, default=200)
     p.add_argument("--only", default="cfg2,cfg3,cfg5")
     p.add_argument("--calibrate", action="store_true",

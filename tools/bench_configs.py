@@ -18,7 +18,7 @@ Each line carries a per-config roofline (algorithmic bytes per kernel and step w
 texture size, HBM fraction per kernel and per step) and, with --pmc, each kernel's measured HBM
 traffic and its ratio to the algorithmic bytes.
 
-usage: python tools/bench_configs.py [--steps 20] [--warmup 5] [--loop-steps 200] [--pmc]
+usage: python tools/bench_configs.py [--steps 50] [--warmup 30] [--loop-steps 200] [--pmc]
 """
 import argparse
 import json

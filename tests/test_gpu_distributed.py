@@ -158,3 +158,44 @@ def test_bench_step_allreduce_matches_128_items(tmp_path, dev):
     bench.step(single)
     part = single["tex"].grad.cpu().numpy()
     assert np.abs(part - want_atlas).max() > 1e-2 * np.abs(want_atlas).max()
+
+
+def _rccl_worker(rank, port, out_dir):
+    """A world of one rank over the "nccl" backend (RCCL): bench.py's N > 1 process-group setup
+    (bench.setup_dist's init_process_group with device_id), one headline step, and RCCL's
+    all_reduce(SUM) and all_gather_into_tensor on its atlas gradient and images."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=1, device_id=dev)
+    try:
+        import bench
+        assert dist.get_backend() == "nccl"
+        w = bench.workload(_bench_args(64), rank, dev)
+        images = bench.step(w)
+        grad = w["tex"].grad.clone()
+        red = w["tex"].grad.clone()
+        dist.all_reduce(red, op=dist.ReduceOp.SUM)
+        out = torch.empty_like(images)
+        dist.all_gather_into_tensor(out, images.detach().contiguous())
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, "rccl.npz"), grad=grad.cpu().numpy(), red=red.cpu().numpy(),
+                 same_images=bool(torch.equal(out, images.detach())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_collectives(tmp_path, dev):
+    """RCCL (the "nccl" backend) on this box: a one-rank process group set up as bench.py sets up its
+    ranks, one headline step, and the two collectives of the N > 1 path on its tensors -- the
+    all_reduce leaves the atlas gradient unchanged (a sum over one rank) and the all_gather returns
+    the images.  The box has one GPU and RCCL refuses two ranks on one device, so this is the RCCL
+    runtime check; the two-rank exchange itself is covered over gloo above."""
+    mp.spawn(_rccl_worker, args=(_free_port(), str(tmp_path)), nprocs=1, join=True)
+    got = np.load(str(tmp_path / "rccl.npz"))
+    assert float(np.abs(got["grad"]).sum()) > 0
+    assert np.array_equal(got["red"], got["grad"])
+    assert bool(got["same_images"])

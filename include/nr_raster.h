@@ -59,7 +59,7 @@ NR_API size_t nr_raster_args_size(void);
 /* ABI version of this header: 5 (NrRasterArgs.face_index_sparse; 4: nr_last_launch; 3: workspace_zeroed of
  * nr_rasterize_backward).
  * Bindings check it, and nr_raster_args_size(), before the first call. */
-#define NR_ABI_VERSION 5
+#define NR_ABI_VERSION 6
 
 /* Scratch bytes needed by the face-index map for B items, F faces, S x S internal pixels
  * (per-face screen bounding boxes + coarse-bin face bitmasks). */
@@ -167,7 +167,25 @@ typedef struct NrRasterArgs {
      * map).  Honoured only with the halo cache and the fused shading; nr_rasterize_backward_params
      * (which reads every entry) refuses such a forward state.  0 = face_index fully written. */
     int face_index_sparse;
+    /* optional, backward only (NR_DRAW_RGB, a texture and texture coordinates shared by the batch):
+     * texture windows that many faces share -- every face of an OBJ's flat-colour material samples
+     * one 2x2 atlas patch (load_obj.py:84-94), so every wave that renders such a material would add
+     * its window into the same texels.  face_hot[f] in [0, num_hot) names the shared window of face f
+     * (faces with identical texture-coordinate triples share it), -1 for the rest; the backward then
+     * adds those faces' window sums into one of NR_HOT_COPIES private copies per hot window in
+     * hot_acc (nr_hot_acc_bytes(num_hot) bytes; zero at the start, like the backward's accumulators:
+     * zeroed by the forward when it lies inside bwd_workspace, otherwise by nr_rasterize_backward
+     * unless workspace_zeroed) and sums the copies into the texture gradient after its main kernel.
+     * num_hot <= NR_HOT_MAX.  NULL / 0 = every window adds into the texture gradient directly (same
+     * results up to the order of float additions). */
+    const int32_t* face_hot;
+    int num_hot;
+    float* hot_acc;
 } NrRasterArgs;
+
+enum { NR_HOT_MAX = 256, NR_HOT_COPIES = 32 };
+/* bytes of NrRasterArgs.hot_acc for num_hot shared windows */
+NR_API size_t nr_hot_acc_bytes(int num_hot);
 
 enum { NR_LIGHT_AMBIENT = 0, NR_LIGHT_DIRECTIONAL = 1, NR_LIGHT_SPECULAR = 2, NR_LIGHT_FLOATS = 8 };
 
@@ -266,7 +284,8 @@ NR_API int nr_profile_read(const char* kernel, float* ms);
  * per lane) and flags = NR_LAUNCH_* bits.  NR_ERR_ARGS when none was recorded. */
 enum { NR_LAUNCH_FUSED_SHADE = 1, NR_LAUNCH_STATIC_CHANNELS = 2, NR_LAUNCH_TWO_PX_PER_LANE = 4,
        NR_LAUNCH_DEEP_FIRST = 8 /* k_raster_fwd: bins dispatched deepest first (k_bin_order) */,
-       NR_LAUNCH_SPLIT = 16 /* k_raster_fwd: deep bins at 1024 threads, the rest at 256 on a side stream */ };
+       NR_LAUNCH_SPLIT = 16 /* k_raster_fwd: deep bins at 1024 threads, the rest at 256 on a side stream */,
+       NR_LAUNCH_HOT_WINDOWS = 32 /* k_raster_bwd: shared texture windows into private copies (face_hot) */ };
 NR_API int nr_last_launch(const char* kernel, int* block_threads, int* flags);
 
 #ifdef __cplusplus

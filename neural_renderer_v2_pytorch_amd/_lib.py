@@ -25,12 +25,14 @@ EXPORTS = [
     "nr_backward_workspace_bytes", "nr_profile_enable", "nr_profile_read",
     "nr_selftest_division", "nr_halo_bytes", "nr_raster_args_size", "nr_rasterize_backward_params",
     "nr_camera_forward", "nr_camera_backward", "nr_camera_workspace_bytes", "nr_texture_packed_bytes",
-    "nr_last_launch",
+    "nr_last_launch", "nr_hot_acc_bytes",
 ]
 
-ABI_VERSION = 5  # include/nr_raster.h NR_ABI_VERSION
+ABI_VERSION = 6  # include/nr_raster.h NR_ABI_VERSION
 
 NR_LAUNCH_FUSED_SHADE, NR_LAUNCH_STATIC_CHANNELS, NR_LAUNCH_TWO_PX_PER_LANE, NR_LAUNCH_DEEP_FIRST, NR_LAUNCH_SPLIT = 1, 2, 4, 8, 16
+NR_LAUNCH_HOT_WINDOWS = 32
+NR_HOT_MAX, NR_HOT_COPIES = 256, 32
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong
 
@@ -53,6 +55,7 @@ class NrRasterArgs(ctypes.Structure):
         ("backgrounds", c_void_p), ("bg_stride_b", c_ll), ("bg_stride_c", c_ll), ("bg_stride_y", c_ll),
         ("grad_backgrounds", c_void_p), ("textures_packed", c_void_p),
         ("bwd_workspace", c_void_p), ("bwd_workspace_bytes", c_size_t), ("face_index_sparse", c_int),
+        ("face_hot", c_void_p), ("num_hot", c_int), ("hot_acc", c_void_p),
     ]
 
 NR_LIGHT_AMBIENT, NR_LIGHT_DIRECTIONAL, NR_LIGHT_SPECULAR, NR_LIGHT_FLOATS = 0, 1, 2, 8
@@ -106,6 +109,8 @@ def lib():
     L.nr_backward_workspace_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int]
     L.nr_raster_args_size.restype = c_size_t
     L.nr_raster_args_size.argtypes = []
+    L.nr_hot_acc_bytes.restype = c_size_t
+    L.nr_hot_acc_bytes.argtypes = [c_int]
     L.nr_halo_bytes.restype = c_size_t
     L.nr_halo_bytes.argtypes = [c_int, c_int, c_int, c_int]
     L.nr_selftest_division.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_void_p]
@@ -115,7 +120,7 @@ def lib():
     for name in EXPORTS:
         if name not in ("nr_last_error", "nr_workspace_bytes", "nr_num_channels", "nr_backward_workspace_bytes",
                         "nr_halo_bytes", "nr_raster_args_size", "nr_camera_workspace_bytes",
-                        "nr_texture_packed_bytes"):
+                        "nr_texture_packed_bytes", "nr_hot_acc_bytes"):
             getattr(L, name).restype = c_int
     # a library of another ABI revision (an NR_LIB_PATH override, a stale build) would misread the
     # arguments (e.g. an older nr_rasterize_backward takes its stream where workspace_zeroed is now)

@@ -100,7 +100,15 @@ struct BwdArgs {
     int F, aa, s, HW;
     float step, inv_step;
     int step_pow2;                     // x / step == x * inv_step exactly
+    // shared texture windows (NrRasterArgs.face_hot): the window sums of a face with face_hot >= 0 go
+    // to private copy (block % NR_HOT_COPIES) of its window in hot_acc, which k_hot_reduce adds into
+    // grad_tex after the kernel; null: every window into grad_tex directly
+    const int32_t* __restrict__ face_hot;
+    int num_hot;
+    float* __restrict__ hot_acc;
 };
+// hot_acc: [NR_HOT_COPIES][num_hot][16 texels][4] window sums, then [num_hot][2] window origins
+__device__ __host__ inline size_t hot_sums_floats(int num_hot) { return (size_t)NR_HOT_COPIES * num_hot * 64; }
 
 // upstream gradient of internal pixel (x, y): the flip / 2x2-mean backward is an index map and /4.
 // gi: this item's [C, s, s] upstream gradient (32-bit offsets inside it)
@@ -673,6 +681,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     // per run, so such hot texels take one atomic per run instead of one per face
     float pend = 0.f;
     int pwx = INT_MIN, pwy = 0;
+    int phid = -1;  // the pending window's shared-window id (face_hot), -1: into the texture gradient
+    const bool hot_on = a.face_hot != nullptr;
+    float* __restrict__ hacc = hot_on ? a.hot_acc + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) & (NR_HOT_COPIES - 1)) * a.num_hot * 64 : nullptr;
+    int* __restrict__ hpos = hot_on ? reinterpret_cast<int*>(a.hot_acc + hot_sums_floats(a.num_hot)) : nullptr;
 #ifdef NR_BWD_TIMING
     int nfaces_dbg = 0;
 #endif
@@ -687,6 +699,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         const int x0w = __builtin_amdgcn_readlane(P[0].wx, l0), x1w = __builtin_amdgcn_readlane(wx1, l1);
         const int y0w = __builtin_amdgcn_readlane(P[0].wy, l0), y1w = __builtin_amdgcn_readlane(wy1, l1);
         const int key = from0 ? k0 : k1, wx = from0 ? x0w : x1w, wy = from0 ? y0w : y1w;
+        const int hid = hot_on ? a.face_hot[key] : -1;
         // key >= 0, so fi == key implies an active pixel
         const unsigned long long m0 = __builtin_amdgcn_ballot_w64(P[0].fi == key) & p0;
         const unsigned long long m1 = __builtin_amdgcn_ballot_w64(fi1 == key) & p1;
@@ -753,9 +766,18 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             const bool tex_lane = want_tex && chunk < 3 && sw && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
             const bool face_lane = chunk == 3 && tt < 9;
             const float fv = face_lane ? v : pend;
-            float* dst = tex_lane ? gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk : gFb + key * 9 + tt;
+            float* tdst = phid >= 0 ? hacc + (phid * 16 + tt) * 4 + chunk : gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk;
+            float* dst = tex_lane ? tdst : gFb + key * 9 + tt;
+            if (tex_lane && phid >= 0 && tt == 0 && chunk == 0) {  // the window's origin (every writer's is the same)
+                hpos[2 * phid] = pwx;
+                hpos[2 * phid + 1] = pwy;
+            }
 #ifdef NR_ABL_NOATOM  // timing builds only: no flush atomics
             if ((tex_lane || face_lane) && fv == 12345.f) unsafeAtomicAdd(dst, fv);
+#elif defined(NR_ABL_NOTEXFLUSH)  // timing builds only: no texture-window flush atomics
+            if (((tex_lane && fv == 12345.f) || face_lane) && fv != 0.f) unsafeAtomicAdd(dst, fv);
+#elif defined(NR_ABL_NOGFFLUSH)  // timing builds only: no face-gradient flush atomics
+            if ((tex_lane || (face_lane && fv == 12345.f)) && fv != 0.f) unsafeAtomicAdd(dst, fv);
 #else
             if ((tex_lane || face_lane) && fv != 0.f) unsafeAtomicAdd(dst, fv);
 #endif
@@ -763,13 +785,19 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
                 pend = sw ? v : pend + v;
                 pwx = wx;
                 pwy = wy;
+                if (sw) phid = hid;
             }
         }
     }
     {  // the last pending window
         const int x = pwx + tdx, y = pwy + tdy;
-        if (want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H && pend != 0.f)
-            unsafeAtomicAdd(gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk, pend);
+        const bool tex_lane = want_tex && chunk < 3 && pwx != INT_MIN && x < sh.tv.W && y < sh.tv.H;
+        if (tex_lane && phid >= 0 && tt == 0 && chunk == 0) {
+            hpos[2 * phid] = pwx;
+            hpos[2 * phid + 1] = pwy;
+        }
+        if (tex_lane && pend != 0.f)
+            unsafeAtomicAdd(phid >= 0 ? hacc + (phid * 16 + tt) * 4 + chunk : gtb + ((int)__umul24(y, sh.tv.W) + x) * 4 + chunk, pend);
     }
     // ---- 5. texture samples outside their face's window (POS_DIRECT): their texel gradients, 4
     // samples per atomic instruction.  Lane (sample u = lane >> 4, row = bit 3, column = bit 2,
@@ -829,6 +857,21 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 #endif
 }
 
+// the private copies of the shared texture windows (BwdArgs.face_hot) summed and added into the RGBA
+// texture-gradient accumulator (item 0: a shared texture): block h = window h, lane (texel t = lane &
+// 15, channel lane >> 4 < 3).  A window no face flushed has sums of 0 and adds nothing.
+__global__ __launch_bounds__(64) void k_hot_reduce(const float* __restrict__ acc, int num_hot, float* __restrict__ gtb,
+                                                   int W, int H) {
+    const int h = blockIdx.x, tt = threadIdx.x & 15, ch = threadIdx.x >> 4;
+    if (ch >= 3) return;
+    const int* pos = reinterpret_cast<const int*>(acc + hot_sums_floats(num_hot));
+    float s = 0.f;
+#pragma unroll 8
+    for (int c = 0; c < NR_HOT_COPIES; c++) s += acc[(((size_t)c * num_hot + h) * 16 + tt) * 4 + ch];
+    const int x = pos[2 * h] + (tt & 3), y = pos[2 * h + 1] + (tt >> 2);
+    if (s != 0.f && x >= 0 && y >= 0 && x < W && y < H) unsafeAtomicAdd(gtb + ((size_t)y * W + x) * 4 + ch, s);
+}
+
 // pixels per lane, per launch: 2 (256 threads) when the grid fills the chip many times over; 1 (512
 // threads, 6 waves/SIMD instead of 4) for small grids, where the waves, not the per-face work, are
 // short (teapot B=4: 0.041 -> 0.035 ms; torus 1024^2 B=1: 0.059 -> 0.048 ms; on the headline and the
@@ -836,18 +879,19 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 template <int FEAT>
 void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
     const bool one = (long long)grid.x * grid.y < 8192;
+    const int hotf = ba.face_hot ? NR_LAUNCH_HOT_WINDOWS : 0;
     if (one) {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
-        g_last_bwd.store(LaunchRec{2 * NT, 0});
+        g_last_bwd.store(LaunchRec{2 * NT, hotf});
     } else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2) {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC>), grid, dim3(NT), 0, st, ba, g, sh);
-        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE});
+        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     } else if (FEAT == 0 && sh.draw == static_draw(4) && ba.aa && ba.step_pow2) {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, 4>), grid, dim3(NT), 0, st, ba, g, sh);
-        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE});
+        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     } else {
         hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
-        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_TWO_PX_PER_LANE});
+        g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     }
 }
 

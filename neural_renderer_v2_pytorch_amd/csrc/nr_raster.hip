@@ -72,12 +72,17 @@ __global__ void k_abl_empty(int) {}
 extern "C" {
 
 const char* nr_last_error(void) { return g_err.c_str(); }
-int nr_version(void) { return 5; }
+int nr_version(void) { return NR_ABI_VERSION; }
 size_t nr_raster_args_size(void) { return sizeof(NrRasterArgs); }
 
 int nr_num_channels(int draw_flags) {
     return ((draw_flags & NR_DRAW_RGB) ? 3 : 0) + ((draw_flags & NR_DRAW_SILHOUETTES) ? 1 : 0) +
            ((draw_flags & NR_DRAW_DEPTH) ? 1 : 0);
+}
+
+size_t nr_hot_acc_bytes(int num_hot) {
+    if (num_hot <= 0) return 0;
+    return align_up(hot_sums_floats(num_hot) * 4) + align_up((size_t)num_hot * 8);
 }
 
 size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
@@ -461,6 +466,11 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     if (rgb && ((long long)a->tex_height * a->tex_width > DIRECT_MAX_HW || a->tex_width >= DIRECT_OFF))
         return fail(NR_ERR_ARGS, "texture gradient: at most %d texels per texture and %d per row (got %d x %d)",
                     DIRECT_MAX_HW, DIRECT_OFF - 1, a->tex_height, a->tex_width);
+    // shared texture windows into private copies (NrRasterArgs.face_hot): a texture and texture
+    // coordinates shared by the batch
+    const bool hot = rgb && tex_items == 1 && a->face_hot && a->num_hot > 0 && !a->vt_batch_stride;
+    if (hot && (a->num_hot > NR_HOT_MAX || !a->hot_acc || ((uintptr_t)a->hot_acc & 15)))
+        return fail(NR_ERR_ARGS, "face_hot: num_hot %d (at most %d) needs a 16-byte aligned hot_acc", a->num_hot, NR_HOT_MAX);
     const size_t need = nr_backward_workspace_bytes(a->batch_size, a->num_faces, a->num_vertices, tex_items,
                                                     a->tex_height, a->tex_width, lit ? a->num_lights : 0);
     if (need > 0 && (!workspace || workspace_bytes < need))
@@ -489,6 +499,14 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
                                  "(the buffer the forward zeroed)", zero_bytes);
     if (zero_bytes > 0 && !prezeroed && hipMemsetAsync(workspace, 0, zero_bytes, st) != hipSuccess)
         return check_launch("hipMemsetAsync");
+    if (hot) {
+        // hot_acc starts at zero: the forward zeroed it when it lies inside the zeroed bwd_workspace
+        const size_t hb = nr_hot_acc_bytes(a->num_hot);
+        const char* hz = (const char*)a->hot_acc;
+        const bool in_zeroed = prezeroed && hz >= (const char*)a->bwd_workspace &&
+                               hz + hb <= (const char*)a->bwd_workspace + a->bwd_workspace_bytes;
+        if (!in_zeroed && hipMemsetAsync(a->hot_acc, 0, hb, st) != hipSuccess) return check_launch("hipMemsetAsync");
+    }
     BwdArgs ba;
     ba.face_records = a->face_records;
     ba.fim = a->face_index;
@@ -508,6 +526,9 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.step = (float)(2. / S);
     ba.inv_step = 1.f / ba.step;
     ba.step_pow2 = (S & (S - 1)) == 0;  // step = 2/S is then a power of two: x / step == x * (S / 2)
+    ba.face_hot = hot ? a->face_hot : nullptr;
+    ba.num_hot = hot ? a->num_hot : 0;
+    ba.hot_acc = hot ? a->hot_acc : nullptr;
     Shade sh = make_shade(a);
     {
         ProfScope _p(P_BWD, st);
@@ -523,6 +544,12 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     }
     e = check_launch("k_raster_bwd");
     if (e) return e;
+    if (hot) {  // before the texture-gradient output (k_vertex_grad / k_tex_out) reads the accumulator
+        hipLaunchKernelGGL(k_hot_reduce, dim3((unsigned)a->num_hot), dim3(64), 0, st, a->hot_acc, a->num_hot, g4,
+                           a->tex_width, a->tex_height);
+        e = check_launch("k_hot_reduce");
+        if (e) return e;
+    }
     const long long nv = (long long)a->batch_size * a->num_vertices;
     if (lit && nv > 0) {
         // lights: vertex-normal gradients -> face normals -> corner gradients (added into gF)

@@ -203,6 +203,42 @@ def _vertex_adjacency(faces_i32, V):
 
 
 _normal_adj = _TensorCache()
+_hot_cache = _TensorCache()
+# a texture window shared by at least this many faces gets private copies in the backward
+# (NrRasterArgs.face_hot): every face of an OBJ's flat-colour material samples one 2x2 atlas patch
+# (load_obj.py:84-94), so all the waves that render the material add into the same texels
+_HOT_MIN_FACES = int(os.environ.get("NR_HOT_MIN_FACES", "32"))
+
+
+def _face_hot(ft, vt_src, dev):
+    """(face_hot [F] int32 on dev, num_hot) for a batch-shared texture-coordinate table vt_src
+    [Vt, 2] and faces_textures ft [F, 3]: faces whose three texture coordinates are identical
+    (bit for bit, so the backward computes the same texel window for all of them) form a group; the
+    NR_HOT_MAX largest groups of at least _HOT_MIN_FACES faces get ids 0.., every other face -1.
+    (None, 0) when no group qualifies.  Cached per (storage, version) of both tensors."""
+    key = (ft.data_ptr(), ft._version, vt_src.data_ptr(), vt_src._version, tuple(ft.shape), tuple(vt_src.shape),
+           _HOT_MIN_FACES, dev)
+    hit = _hot_cache.get(key)
+    if hit is not None:
+        return hit[0], hit[1]
+    import numpy as np
+    if _HOT_MIN_FACES <= 0 or ft.shape[0] == 0:
+        res = (None, 0)
+    else:
+        uv = vt_src.detach().float().cpu().numpy()[ft.long().cpu().numpy()]  # [F, 3, 2]
+        rows = np.ascontiguousarray(uv.reshape(-1, 6)).view(np.int32)        # exact bits
+        _, inv, cnt = np.unique(rows, axis=0, return_inverse=True, return_counts=True)
+        inv = inv.reshape(-1)
+        big = np.nonzero(cnt >= _HOT_MIN_FACES)[0]
+        big = big[np.argsort(-cnt[big], kind="stable")][:_lib.NR_HOT_MAX]
+        if len(big) == 0:
+            res = (None, 0)
+        else:
+            ids = np.full(len(cnt), -1, np.int32)
+            ids[big] = np.arange(len(big), dtype=np.int32)
+            res = (torch.as_tensor(ids[inv], device=dev), len(big))
+    _hot_cache.put(key, (res[0], res[1], ft, vt_src))  # keep the key tensors alive
+    return res[0], res[1]
 
 
 def _normal_adjacency(faces_i32, V):
@@ -323,9 +359,9 @@ class _Layout:
     them needs a tensor of its own: one caching-allocator call per forward instead of up to eight.
     Computed once per configuration (sizes only) and cached."""
     __slots__ = ("nbytes", "frec", "fuv", "ws", "ws_bytes", "halo", "halo_bytes", "tex4", "bws", "bws_bytes",
-                 "fnorm", "vnorm", "bwd_need")
+                 "fnorm", "vnorm", "bwd_need", "hot", "num_hot")
 
-    def __init__(self, L, cfg, uv_items, want_halo, want_bws, tex_grad, nl):
+    def __init__(self, L, cfg, uv_items, want_halo, want_bws, tex_grad, nl, num_hot=0):
         off = 0
 
         def take(n):
@@ -355,8 +391,18 @@ class _Layout:
         tex_items = (1 if cfg.tex_shared else B) if (rgb and tex_grad) else 0
         # the backward's workspace for this configuration (its texture gradient follows tex_grad)
         self.bwd_need = L.nr_backward_workspace_bytes(B, F, V, tex_items, H, W, nl)
+        # the shared windows' private copies (NrRasterArgs.hot_acc) right after the backward's
+        # workspace, inside the span the forward zeroes
+        self.num_hot = num_hot
+        hot_bytes = L.nr_hot_acc_bytes(num_hot) if num_hot > 0 else 0
+        self.hot = None
         if want_bws and self.bwd_need <= _BWD_PREZERO_MAX:
-            self.bws, self.bws_bytes = take(self.bwd_need), self.bwd_need
+            self.bws = take(self.bwd_need)
+            if hot_bytes:
+                self.hot = take(hot_bytes)
+            self.bws_bytes = off - self.bws
+        elif hot_bytes:
+            self.hot = take(hot_bytes)  # zeroed by the backward
         self.fnorm = self.vnorm = None
         if nl:
             self.fnorm, self.vnorm = take(B * F * 3 * 4), take(B * V * 4 * 4)
@@ -374,6 +420,8 @@ class _Layout:
             a.textures_packed = base + self.tex4
         if self.bws is not None:
             a.bwd_workspace, a.bwd_workspace_bytes = base + self.bws, self.bws_bytes
+        if self.hot is not None:
+            a.hot_acc, a.num_hot = base + self.hot, self.num_hot
         if self.fnorm is not None:
             a.face_normals, a.vertex_normals = base + self.fnorm, base + self.vnorm
 
@@ -381,14 +429,14 @@ class _Layout:
 _layouts = {}
 
 
-def _layout(L, cfg, uv_items, want_halo, want_bws, tex_grad, nl):
+def _layout(L, cfg, uv_items, want_halo, want_bws, tex_grad, nl, num_hot=0):
     key = (cfg.B, cfg.F, cfg.V, cfg.image_size, cfg.aa, cfg.flags, cfg.tex_hw, cfg.tex_shared, uv_items,
-           want_halo, want_bws, tex_grad, nl, _TEX_PACK)
+           want_halo, want_bws, tex_grad, nl, _TEX_PACK, num_hot)
     lay = _layouts.get(key)
     if lay is None:
         if len(_layouts) > 64:
             _layouts.clear()
-        lay = _layouts[key] = _Layout(L, cfg, uv_items, want_halo, want_bws, tex_grad, nl)
+        lay = _layouts[key] = _Layout(L, cfg, uv_items, want_halo, want_bws, tex_grad, nl, num_hot)
     return lay
 
 
@@ -421,13 +469,21 @@ class Rasterize(torch.autograd.Function):
         grads = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         uv_items = (1 if vt_bstride == 0 else B) if rgb else 0
         nl = light_recs.shape[0] if light_recs is not None else 0
+        # shared texture windows (a texture and texture coordinates shared by the batch, texture gradient wanted)
+        face_hot, num_hot = None, 0
+        if rgb and ctx.needs_input_grad[1] and cfg.tex_shared and vt_bstride == 0:
+            face_hot, num_hot = _face_hot(faces_textures, vertices_textures[0] if vertices_textures.ndim == 3
+                                          else vertices_textures, dev)
         lay = _layout(L, cfg, uv_items, _HALO_CACHE and grads, _BWD_PREZERO and grads,
-                      ctx.needs_input_grad[1], nl)
+                      ctx.needs_input_grad[1], nl, num_hot)
         arena = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
         fim = torch.empty((B, S, S), dtype=torch.int32, device=dev)
         images = torch.empty((B, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev)
         a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, fim, vt_bstride)
         lay.fill(a, arena.data_ptr())
+        if face_hot is not None:
+            a.face_hot = face_hot.data_ptr()
+            ctx.face_hot = face_hot  # alive until the backward
         if _FIM_FILL is not None:
             fim.fill_(_FIM_FILL)
         if _HALO_FILL is not None and lay.halo is not None:
@@ -493,7 +549,7 @@ class Rasterize(torch.autograd.Function):
             gt = torch.empty((tex_items, 3, H, W), dtype=torch.float32, device=dev)
         lay = ctx.layout
         need = lay.bwd_need
-        prezeroed = ctx.prezeroed and lay.bws_bytes == need
+        prezeroed = ctx.prezeroed and lay.bws is not None
         ctx.prezeroed = False
         if prezeroed:
             ws_ptr = a.bwd_workspace  # the library checks it is the buffer the forward zeroed

@@ -161,8 +161,11 @@ def test_cfg3_car_subdivided_vs_oracle(car64, q):
     forward (1024-thread deep prefix, deepest bin first; asserted from the library's launch
     record); they hold more than one 512-face staging round."""
     assert car64["launch"] == (1024, _lib.NR_LAUNCH_FUSED_SHADE | _lib.NR_LAUNCH_DEEP_FIRST | _lib.NR_LAUNCH_SPLIT)
-    # rgba (rgb + silhouettes): the backward's compile-time 4-channel instantiation
-    assert car64["bwd_launch"] == (256, _lib.NR_LAUNCH_STATIC_CHANNELS | _lib.NR_LAUNCH_TWO_PX_PER_LANE)
+    # rgba (rgb + silhouettes): the backward's compile-time 4-channel instantiation, with the car's
+    # shared texture windows (faces with identical texture coordinates, e.g. every face of a
+    # flat-colour material, sample one patch) summed in private copies (face_hot)
+    assert car64["bwd_launch"] == (256, _lib.NR_LAUNCH_STATIC_CHANNELS | _lib.NR_LAUNCH_TWO_PX_PER_LANE |
+                                   _lib.NR_LAUNCH_HOT_WINDOWS)
     if q == 0:
         counts = _bin_candidates(car64["proj"][:4], car64["f"], 512)
         assert counts.max() > 512, counts.max()

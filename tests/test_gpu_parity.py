@@ -1290,3 +1290,50 @@ def test_pixel_centre_division(dev):
         assert not bad.any(), (int(bad.sum()), a[bad][:4].tolist(), b[bad][:4].tolist())
         done += n
     assert done > 134000000
+
+
+def test_shared_texture_windows_vs_oracle(oracle_mod, dev):
+    """Texture windows shared by many faces (NrRasterArgs.face_hot): three groups of faces with
+    identical texture-coordinate triples, each a flat-colour-material patch of load_obj.py:84-94
+    ([0, p], [0, p + 1], [1, p + 1] in texel units), on a texture shared by the batch.  The backward
+    sums those windows in private copies and adds them into the texture gradient after its main
+    kernel (asserted from its launch record).  The atlas gradient matches the oracle's sum over the
+    batch, equals the direct path's (face_hot off) within the tolerance, and a second backward
+    through the same graph (its accumulators, the private copies among them, zeroed by the backward
+    itself this time) adds the same gradient again."""
+    B, s = 4, 64
+    proj, f = _ico_batch(3, B, dev)
+    faces = torch.as_tensor(f, device=dev)
+    vt = np.array([[[0, p], [0, p + 1], [1, p + 1]] for p in (0, 2, 4)], np.float32).reshape(-1, 2)
+    ft = np.stack([np.arange(3) + 3 * (i % 3) for i in range(f.shape[0])]).astype(np.int32)
+    tex = np.random.RandomState(81).uniform(0, 1, (3, 8, 8)).astype(np.float32)
+    g = torch.as_tensor(np.random.RandomState(82).normal(size=(B, 5, s, s)).astype(np.float32), device=dev)
+
+    def run(min_faces):
+        old = nrr._HOT_MIN_FACES
+        nrr._HOT_MIN_FACES = min_faces
+        try:
+            v = proj.detach().to(dev).requires_grad_(True)
+            t = torch.as_tensor(tex, device=dev).requires_grad_(True)
+            params = nr.RasterizeParam(vertices_textures=torch.as_tensor(vt, device=dev)[None].expand(B, -1, -1),
+                                       faces_textures=torch.as_tensor(ft, device=dev),
+                                       textures=t[None].expand(B, -1, -1, -1))
+            img = nrr.rasterize_core(v, faces, params, nr.RasterizeHyperparam(image_size=s))
+            img.backward(g, retain_graph=True)
+            launch = _lib.last_launch("k_raster_bwd")
+            first = (v.grad.clone(), t.grad.clone())
+            img.backward(g)
+            return launch, first, (v.grad.clone(), t.grad.clone())
+        finally:
+            nrr._HOT_MIN_FACES = old
+    launch, (gv, gt), (gv2, gt2) = run(32)
+    assert launch[1] & _lib.NR_LAUNCH_HOT_WINDOWS
+    launch0, (gv0, gt0), _ = run(0)
+    assert not launch0[1] & _lib.NR_LAUNCH_HOT_WINDOWS
+    assert float(gt.abs().sum()) > 0
+    close_grads(gt, gt0, "shared windows vs direct: grad textures")
+    close_grads(gv, gv0, "shared windows vs direct: grad vertices")
+    close_grads(gt2, 2 * gt, "second backward: grad textures")
+    _, _, rgv, rgt = oracle_batch(oracle_mod, proj, f, g, s, torch.as_tensor(tex), vt, ft)
+    close_grads(gt, rgt, "shared windows: grad textures vs oracle")
+    close_grads(gv, rgv, "shared windows: grad vertices vs oracle")

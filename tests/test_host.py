@@ -96,7 +96,9 @@ def test_library_exports_every_header_symbol():
     L = ctypes.CDLL(_lib.LIB_PATH)
     for name in declared:
         assert hasattr(L, name), name
-    assert _lib.lib().nr_version() == _lib.ABI_VERSION == 5
+    assert _lib.lib().nr_version() == _lib.ABI_VERSION == 6
+    assert _lib.lib().nr_hot_acc_bytes(0) == 0
+    assert _lib.lib().nr_hot_acc_bytes(3) >= _lib.NR_HOT_COPIES * 3 * 64 * 4 + 3 * 8
     # the ctypes mirror of NrRasterArgs has the C layout
     assert _lib.lib().nr_raster_args_size() == ctypes.sizeof(_lib.NrRasterArgs)
     assert _lib.lib().nr_num_channels(7) == 5 and _lib.lib().nr_num_channels(2) == 1

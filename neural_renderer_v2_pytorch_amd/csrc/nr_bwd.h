@@ -217,7 +217,10 @@ struct BwdPix {
 // (rgb + sil + depth, C = MAXC) the per-channel `c < C` guards of the loads, the LDS staging and the
 // stencil fold away, with their zero defaults and scalar branches; that instantiation is launched
 // only with anti-aliasing and a power-of-two raster (both folded too).
-template <int FEAT, int NPX, int CC = 0>
+// HOT: the shared-window flush (BwdArgs.face_hot) compiled in; its instantiations run only when the
+// caller passes face_hot (its per-face id load and address select cost the headline's backward 4 %,
+// 0.194 -> 0.202 ms, when compiled into the plain instantiation, gpurun_out/nh)
+template <int FEAT, int NPX, int CC = 0, bool HOT = false>
 __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? 6 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
     constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0, SILO = (FEAT & 4) != 0;
     // features this instantiation does not have become compile-time constants (the shared
@@ -682,7 +685,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     float pend = 0.f;
     int pwx = INT_MIN, pwy = 0;
     int phid = -1;  // the pending window's shared-window id (face_hot), -1: into the texture gradient
-    const bool hot_on = a.face_hot != nullptr;
+    const bool hot_on = HOT && a.face_hot != nullptr;
     float* __restrict__ hacc = hot_on ? a.hot_acc + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) & (NR_HOT_COPIES - 1)) * a.num_hot * 64 : nullptr;
     int* __restrict__ hpos = hot_on ? reinterpret_cast<int*>(a.hot_acc + hot_sums_floats(a.num_hot)) : nullptr;
 #ifdef NR_BWD_TIMING
@@ -876,23 +879,35 @@ __global__ __launch_bounds__(64) void k_hot_reduce(const float* __restrict__ acc
 // threads, 6 waves/SIMD instead of 4) for small grids, where the waves, not the per-face work, are
 // short (teapot B=4: 0.041 -> 0.035 ms; torus 1024^2 B=1: 0.059 -> 0.048 ms; on the headline and the
 // car the smaller wave regions mean more face flushes: 0.405 -> 0.417 and 0.73 -> 0.84 ms).
-template <int FEAT>
-void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
+template <int FEAT, bool HOT>
+void launch_bwd_v(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
     const bool one = (long long)grid.x * grid.y < 8192;
-    const int hotf = ba.face_hot ? NR_LAUNCH_HOT_WINDOWS : 0;
+    const int hotf = HOT ? NR_LAUNCH_HOT_WINDOWS : 0;
     if (one) {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 1>), grid, dim3(2 * NT), 0, st, ba, g, sh);
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 1, 0, HOT>), grid, dim3(2 * NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{2 * NT, hotf});
     } else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2) {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC>), grid, dim3(NT), 0, st, ba, g, sh);
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     } else if (FEAT == 0 && sh.draw == static_draw(4) && ba.aa && ba.step_pow2) {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, 4>), grid, dim3(NT), 0, st, ba, g, sh);
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, 4, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     } else {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2>), grid, dim3(NT), 0, st, ba, g, sh);
+        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, 0, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     }
+}
+// the shared-window instantiations exist for the plain textured backward (FEAT 0) only; the caller
+// passes face_hot for no other (nr_rasterize_backward)
+template <int FEAT>
+void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
+    if constexpr (FEAT == 0) {
+        if (ba.face_hot) {
+            launch_bwd_v<FEAT, true>(grid, st, ba, g, sh);
+            return;
+        }
+    }
+    launch_bwd_v<FEAT, false>(grid, st, ba, g, sh);
 }
 
 constexpr int VGRAD_UNROLL = 4;

@@ -684,7 +684,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     NR_FTSTAMP(0, clock64());
     NR_FTSTAMP(8, wall_clock64());
 #ifdef NR_FWD_TIMING
-    unsigned long long t_stage = 0;
+    unsigned long long t_stage = 0, t_wait = 0;  // staging rounds; (static blocks) waits after the walks
 #endif
     // the first round of mask words and its candidate count
     const uint32_t bits0 = (!known_empty && t < g.nwords) ? words[t] : 0u;
@@ -822,7 +822,13 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                             walk_block<FCAP, false>(s_face, s_bm, ublk[k], n, lane, xp[k], yp[k], near, far, delta,
                                                     depth_min[k], best[k]);
                     }
+#ifdef NR_FWD_TIMING
+                    const unsigned long long tw0_ = clock64();
+#endif
                     __syncthreads();
+#ifdef NR_FWD_TIMING
+                    t_wait += clock64() - tw0_;
+#endif
                 }
             }
             wbase += NTF;
@@ -852,6 +858,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 
     NR_FTSTAMP(3, clock64());
     NR_FTSTAMP(2, t_stage);
+    NR_FTSTAMP(7, t_wait);
     // may the bin hold a foreground pixel (the backward skips its tiles when not): a bin without
     // candidate faces holds none
     if (binfg && t == 0) binfg[(long long)b * g.nbins + bin] = ncand > 0 ? 1 : 0;

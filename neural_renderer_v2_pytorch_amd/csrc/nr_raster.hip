@@ -468,7 +468,10 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
                     DIRECT_MAX_HW, DIRECT_OFF - 1, a->tex_height, a->tex_width);
     // shared texture windows into private copies (NrRasterArgs.face_hot): a texture and texture
     // coordinates shared by the batch
-    const bool hot = rgb && tex_items == 1 && a->face_hot && a->num_hot > 0 && !a->vt_batch_stride;
+    // (the plain textured backward only: no lights, no backgrounds -- their instantiations have no
+    // shared-window flush -- and rgb drawn)
+    const bool hot = rgb && tex_items == 1 && a->face_hot && a->num_hot > 0 && !a->vt_batch_stride && !lit &&
+                     !a->backgrounds;
     if (hot && (a->num_hot > NR_HOT_MAX || !a->hot_acc || ((uintptr_t)a->hot_acc & 15)))
         return fail(NR_ERR_ARGS, "face_hot: num_hot %d (at most %d) needs a 16-byte aligned hot_acc", a->num_hot, NR_HOT_MAX);
     const size_t need = nr_backward_workspace_bytes(a->batch_size, a->num_faces, a->num_vertices, tex_items,

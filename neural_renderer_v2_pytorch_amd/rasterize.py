@@ -345,6 +345,7 @@ _BWD_PREZERO = os.environ.get("NR_BWD_PREZERO", "1") != "0"
 # grad-enabled forward whose backward never runs (a render kept for logging, validation without
 # no_grad) still allocates and zero-fills the workspace, and holds it as long as its graph lives.
 _BWD_PREZERO_MAX = 32 << 20
+_WS_ARENA_MAX = 16 << 20
 _TEX_PACK_MAX_BYTES = 1 << 31
 
 
@@ -375,7 +376,9 @@ class _Layout:
         self.frec = take(B * F * 16 * 4)
         self.fuv = take(uv_items * F * 8 * 4) if rgb else None
         self.ws_bytes = L.nr_workspace_bytes(B, F, S)
-        self.ws = take(self.ws_bytes)
+        # the forward's bin workspace is read by the forward only: in the arena (which the graph keeps
+        # alive until its backward) when small, else a temporary freed when the forward returns
+        self.ws = take(self.ws_bytes) if self.ws_bytes <= _WS_ARENA_MAX else None
         self.halo = self.halo_bytes = None
         if want_halo:
             self.halo_bytes = L.nr_halo_bytes(B, cfg.image_size, int(cfg.aa), cfg.flags)
@@ -413,7 +416,8 @@ class _Layout:
         a.face_records = base + self.frec
         if self.fuv is not None:
             a.face_uv = base + self.fuv
-        a.workspace, a.workspace_bytes = base + self.ws, self.ws_bytes
+        if self.ws is not None:
+            a.workspace, a.workspace_bytes = base + self.ws, self.ws_bytes
         if self.halo is not None:
             a.halo = base + self.halo
         if self.tex4 is not None:
@@ -481,6 +485,10 @@ class Rasterize(torch.autograd.Function):
         images = torch.empty((B, cfg.C, cfg.image_size, cfg.image_size), dtype=torch.float32, device=dev)
         a = _args(cfg, vertices, faces, vertices_textures, faces_textures, textures, fim, vt_bstride)
         lay.fill(a, arena.data_ptr())
+        ws_tmp = None
+        if lay.ws is None:  # a large bin workspace: a temporary (stream-ordered reuse once it is freed)
+            ws_tmp = torch.empty(lay.ws_bytes, dtype=torch.uint8, device=dev)
+            a.workspace, a.workspace_bytes = ws_tmp.data_ptr(), lay.ws_bytes
         if face_hot is not None:
             a.face_hot = face_hot.data_ptr()
             ctx.face_hot = face_hot  # alive until the backward
@@ -506,6 +514,9 @@ class Rasterize(torch.autograd.Function):
                                   light_recs is None and not (rgb and ctx.needs_input_grad[2]))
         with _lib.on_device(dev):
             _lib.check(L.nr_rasterize_forward(a, images.data_ptr(), _lib.stream_of(vertices)), "nr_rasterize_forward")
+        if ws_tmp is not None:
+            a.workspace, a.workspace_bytes = None, 0
+            del ws_tmp
         # the backward's workspace was zeroed by the setup launch (NrRasterArgs.bwd_workspace): for the
         # first backward only (its accumulators are spent after it)
         ctx.prezeroed = lay.bws is not None

@@ -3,7 +3,9 @@ variant) or the car (--workload car: the split forward, its deep launch at 1024 
 at 256 on a side stream, each decoded with its own block size) (timing build, NR_FWD_TIMING).
 usage (GPU box): python tools/fwd_timing.py [--workload car|cfg2] [extra -D flags...]
 Phases: mask words + candidate scan, face staging rounds (summed), candidate expansion + face walk,
-fim write + bin flag + LDS hand-over, shading epilogue; split by the bin's candidate count."""
+the wait at the barrier after each staging round's walks (static blocks: a wave that finished its
+block waits for the round's slowest), fim write + bin flag + LDS hand-over, shading epilogue; split by
+the bin's candidate count."""
 import ctypes
 import os
 import subprocess
@@ -75,9 +77,10 @@ def report(t):
     blocks = t.shape[0]
     nc = t[:, 0, 6]
     st = t[:, :, 2]  # cycles in the staging rounds (face loads + LDS stores + barrier), summed
-    ph = np.stack([t[:, :, 1] - t[:, :, 0], st, t[:, :, 3] - t[:, :, 1] - st,
+    wt = t[:, :, 7]  # (static blocks) cycles at the barrier after each round's walks, summed
+    ph = np.stack([t[:, :, 1] - t[:, :, 0], st, t[:, :, 3] - t[:, :, 1] - st - wt, wt,
                    t[:, :, 4] - t[:, :, 3], t[:, :, 5] - t[:, :, 4]], axis=2)
-    names = ["scan", "stage", "walk", "fim+flag", "shade"]
+    names = ["scan", "stage", "walk", "walk-wait", "fim+flag", "shade"]
     life = t[:, :, 5] - t[:, :, 0]
     print("blocks %d; candidates per bin: zero in %.1f%%, mean %.1f over the rest" % (
         blocks, 100 * (nc == 0).mean(), nc[nc > 0].mean() if (nc > 0).any() else 0))

@@ -369,8 +369,12 @@ template <int NTF> struct FwdCfg {
     static constexpr int NSUB = (COARSE * COARSE) / NTF;       // 8x8 blocks (pixels) per thread
     static constexpr int CAND = NTF >= 1024 ? 1024 : 512;      // candidate ids expanded per round
     static constexpr int FCAP = NTF >= 1024 ? 512 : 160;       // faces staged per round
-    // staged records, candidate ids (dyn + SHADE: then the winners' staging slots), block masks
-    static constexpr int LDS = FCAP * FREC * 16 + CAND * 4 + FCAP * 2 + 16 * 4;
+    // staged records, candidate ids (dyn + SHADE: then the winners' staging slots), block masks, block
+    // extents; (1024 threads) the dealt-quarter walk's quarter masks, quarter extents, per-pixel state
+    // and per-quarter counts / order
+    static constexpr int LDS_BASE = FCAP * FREC * 16 + CAND * 4 + FCAP * 2 + 16 * 4;
+    static constexpr int LDS_DQ = NTF >= 1024 ? FCAP * 8 + 32 * 4 + COARSE * COARSE * 8 + 64 * 4 * 2 : 0;
+    static constexpr int LDS = LDS_BASE + LDS_DQ;
     // 8x8 block k of wave w: its origin (ox, oy) in the bin
     __device__ static __forceinline__ void block_of(int w, int k, int& ox, int& oy) {
         if (NSUB == 1) {         // 16 waves: wave w owns block (w & 3, w >> 2)
@@ -463,8 +467,8 @@ constexpr int ZCULL_MIN = 512;  // candidates of a bin (first bin-mask round)
 // one wave's walk of the n staged faces over its 8x8 block u of the bin (pixel (xp, yp) per lane): the
 // ballot takes the staged faces whose block mask (face_block_mask: bbox, and with CULL the edge cull)
 // has bit u, then the per-face test runs in ascending order
-template <int FST, bool SLOT, bool ZCULL = false>
-__device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, const uint16_t* __restrict__ s_bm, int u,
+template <int FST, bool SLOT, bool ZCULL = false, typename MT = uint16_t, bool Q16 = false>
+__device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, const MT* __restrict__ s_bm, int u,
                                            int n, int lane, float xp, float yp, float near, float far, float delta,
                                            float& depth_min, int& best) {
     int pend = -1;               // staging slot of my pixel's pending face
@@ -501,8 +505,10 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, co
             // each comparison straight to a lane mask (v_cmp into an SGPR pair; the masks combine on the
             // scalar unit): a ballot of the combined boolean costs a v_cndmask + v_cmp per face to
             // rebuild the mask.  !(a < b) is "a >= b or unordered" (UGE), !(a > b) is ULE.
+            // (Q16: a 4x4 quarter, lanes 0-15 only)
             const unsigned long long pre = lane_mask_uge(depth_min, q1.x) & lane_mask_uge(xp, q0.x) &
-                                           lane_mask_ule(xp, q0.y) & lane_mask_uge(yp, q0.z) & lane_mask_ule(yp, q0.w);
+                                           lane_mask_ule(xp, q0.y) & lane_mask_uge(yp, q0.z) & lane_mask_ule(yp, q0.w) &
+                                           (Q16 ? 0xffffull : ~0ull);
             unsigned long long cov = 0;
             if (pre) {
                 // .cu:107-116: c1 = (yp - y0) A - B (xp - x0), c3 = (yp - y2) E - F (xp - x2),
@@ -570,11 +576,48 @@ __device__ __forceinline__ void block_extents(float* ext, int t, int bx0, int by
     }
 }
 
+// The bin's 64 4x4 quarters (quarter q = 8 R + J: column J, row R), for the dealt-quarter deep walk:
+// thread t < 32 writes extent t ([0..7] x lo, [8..15] x hi, [16..23] y lo, [24..31] y hi per quarter
+// column / row), and face_quarter_mask gives quarter rows r0 .. r0 + 3 of a face's mask (bit
+// 8 (R - r0) + J): the bbox test and, with CULL, the edge cull (nr_block_culled, exact for any
+// rectangle of pixel centres), as face_block_mask does for the 8x8 blocks
+__device__ __forceinline__ void quarter_extents(float* ext4, int t, int bx0, int by0, int S) {
+    if (t < 32) {
+        const int base = (t & 16) ? by0 : bx0, j = t & 7;
+        ext4[t] = pix_center(base + 4 * j + ((t & 8) ? 3 : 0), S);
+    }
+}
+template <bool CULL>
+__device__ __forceinline__ uint32_t face_quarter_mask(const float* __restrict__ c, const float* __restrict__ ext4, int r0) {
+    const float x0 = c[0], y0 = c[1], x1 = c[3], y1 = c[4], x2 = c[6], y2 = c[7];
+    const float xmin = fminf(fminf(x0, x1), x2), xmax = fmaxf(fmaxf(x0, x1), x2);
+    const float ymin = fminf(fminf(y0, y1), y2), ymax = fmaxf(fmaxf(y0, y1), y2);
+    uint32_t mx = 0, m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) mx |= (!(ext4[8 + j] < xmin || ext4[j] > xmax) ? 1u : 0u) << j;
+#pragma unroll
+    for (int r = 0; r < 4; r++) m |= !(ext4[24 + r0 + r] < ymin || ext4[16 + r0 + r] > ymax) ? mx << (8 * r) : 0u;
+    // (the edge cull per quarter: culling per 8x8 block and spreading each block's bit over its
+    // quarters halved the staging's culls, but the longer lists cost the torus forward more, 0.114 ->
+    // 0.118 ms, gpurun_out/dq2)
+    if (CULL) {
+        const float A = x1 - x0, B = y1 - y0, C = x2 - x1, D = y2 - y1, E = x0 - x2, F = y0 - y2;
+        for (uint32_t rest = m; rest; rest &= rest - 1) {
+            const int bit = __builtin_ctz(rest), j = bit & 7, r = r0 + (bit >> 3);
+            const float xl = ext4[j], xh = ext4[8 + j], yl = ext4[16 + r], yh = ext4[24 + r];
+            if (nr_block_culled(x0, y0, x1, y1, x2, y2, A, B, C, D, E, F, 0.5f * (xl + xh), 0.5f * (yl + yh),
+                                0.5f * (xh - xl), 0.5f * (yh - yl)))
+                m &= ~(1u << bit);
+        }
+    }
+    return m;
+}
+
 // stage staged-face slot `slot` of candidate face f (coordinates c) and its block mask.  half (the
 // 1024-thread variant: twice as many threads as staged faces): thread `slot` evaluates the mask's
 // block rows 0-1 and thread FST + slot rows 2-3 (stage_mask_rows), each writing its byte, so the edge
 // culls of a round spread over every wave of the block.
-template <int FST, bool CULL>
+template <int FST, bool CULL, bool MASK = true>
 __device__ __forceinline__ void stage_face(float4* s_face, uint16_t* s_bm, int slot, const float* __restrict__ c, int f,
                                            const float* __restrict__ ext, bool half) {
     float4* e = s_face + slot;
@@ -583,9 +626,11 @@ __device__ __forceinline__ void stage_face(float4* s_face, uint16_t* s_bm, int s
     const float xmin = fminf(fminf(x0, x1), x2), xmax = fmaxf(fmaxf(x0, x1), x2);
     const float ymin = fminf(fminf(y0, y1), y2), ymax = fmaxf(fmaxf(y0, y1), y2);
     e[0 * FST] = make_float4(xmin, xmax, ymin, ymax);
-    const uint32_t m = face_block_mask<CULL>(x0, y0, x1, y1, x2, y2, xmin, xmax, ymin, ymax, ext, 0, half ? 2 : 4);
-    if (half) reinterpret_cast<uint8_t*>(s_bm)[2 * slot] = (uint8_t)m;
-    else s_bm[slot] = (uint16_t)m;
+    if (MASK) {
+        const uint32_t m = face_block_mask<CULL>(x0, y0, x1, y1, x2, y2, xmin, xmax, ymin, ymax, ext, 0, half ? 2 : 4);
+        if (half) reinterpret_cast<uint8_t*>(s_bm)[2 * slot] = (uint8_t)m;
+        else s_bm[slot] = (uint16_t)m;
+    }
     e[1 * FST] = make_float4(fminf(fminf(z0, z1), z2), x1 * y2 - x2 * y1, x0 * y1 - x1 * y0, x2 * y0 - x0 * y2);
     e[2 * FST] = make_float4(y0, y2, x0, x2);
     e[3 * FST] = make_float4(x1 - x0, x0 - x2, y1 - y0, y0 - y2);
@@ -635,7 +680,10 @@ constexpr int FWD_WPE = 8;
 // CC (SHADE only): the channel count as a compile-time constant; CC = MAXC means rgb + sil + depth, 4
 // rgb + sil (static_draw), so the epilogue's draw-flag tests and per-channel guards fold away (0: sh.C /
 // sh.draw at run time)
-template <int NTF, bool SHADE, int CC = 0>
+// DQ (1024 threads): the dealt-quarter walk for bins of >= ZCULL_MIN candidates compiled in (its own
+// instantiation: in the static-blocks kernel its registers and LDS cost the car's split deep launch
+// 1.3 %, gpurun_out/dq3)
+template <int NTF, bool SHADE, int CC = 0, bool DQ = false>
 __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8))) void k_raster_fwd(const float* __restrict__ face_records, int rs,
                                                   const int2* __restrict__ bbox, const uint32_t* __restrict__ mask,
                                                   int F, Geom g, float near, float far, float delta,
@@ -652,7 +700,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     // variant (headline forward 0.1444 -> 0.1397 ms, torus 0.1207 -> 0.1181 ms, the car unchanged;
     // same-box A/B, 3 runs each, gpurun_out/e3)
     constexpr bool CULL = true;
-    __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS];
+    __shared__ __attribute__((aligned(16))) unsigned char s_raw[C::LDS_BASE + (DQ ? C::LDS_DQ : 0)];
     __shared__ int s_scan[C::NW];
     __shared__ int s_next;  // (dyn) next 8x8 block to walk
     float4* s_face = reinterpret_cast<float4*>(s_raw);
@@ -762,6 +810,129 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                 const int px = bx0 + ox + (lane & 7), py = by0 + oy + (lane >> 3);
                 if (px < S && py < S) fimb[(int)__umul24(py, S) + px] = id;
             }
+        }
+    } else if (DQ && NTF >= 1024 && CULL && total0 >= ZCULL_MIN) {
+        // dealt quarters (the deep bins of the 1024-thread variant): in each staging round the bin's 64
+        // 4x4 quarters, longest face list first, are dealt to the 16 waves from a counter; a wave walks
+        // one quarter at a time on lanes 0-15, its pixels' state (depth, winner) in LDS between rounds.
+        // With one 8x8 block per wave for the whole bin, the waves of the car's deep bins spent 65 % of
+        // their walk phase waiting at each round's barrier for the round's heaviest block (timing build,
+        // profiles/r05_v59_car_fwd_wave_phases.txt: walk 130k, wait 249k cycles per wave); dealt
+        // quarters cut a round's span to 0.61x of the heaviest block's walk (CPU model of the car's
+        // deep bins: the quarters' lists are 0.45x a block's, and the waves share them out).  They walk
+        // ~1.8x the face-quarter pairs, though, and stage 64 quarter masks per face: in the split
+        // forward's deep launch (part 1, the car) the deep bins then ended at 378 instead of 435 us but
+        // took wave slots from the concurrent rest launch, which ended 27 us later (forward 0.442 ->
+        // 0.446-0.454 ms); where the deep bins have the chip to themselves (one item: the 50k torus)
+        // the forward went 0.134 -> 0.114 ms (gpurun_out/dq, dq2)
+        constexpr int QD = C::LDS_BASE;
+        uint64_t* s_q = reinterpret_cast<uint64_t*>(s_raw + QD);                       // staged faces' quarter masks
+        float* s_ext4 = reinterpret_cast<float*>(s_raw + QD + FCAP * 8);              // quarter extents
+        float* s_dm = reinterpret_cast<float*>(s_raw + QD + FCAP * 8 + 128);          // per-pixel depth (py 32 + px)
+        int* s_best = reinterpret_cast<int*>(s_raw + QD + FCAP * 8 + 128 + COARSE * COARSE * 4);
+        int* s_qc = s_best + COARSE * COARSE;                                          // per-quarter walk lengths
+        int* s_qord = s_qc + 64;                                                       // quarters, longest first
+        s_dm[t] = far;
+        s_best[t] = -1;
+        quarter_extents(s_ext4, t, bx0, by0, S);
+        uint32_t bits = bits0;
+        int total = total0, off = off0;
+        for (int wbase = 0;;) {
+            const int w = wbase + t;
+            ncand += total;
+            for (int cbase = 0; cbase < total; cbase += CAND) {
+                int r = off;
+                for (uint32_t m = bits; m; m &= m - 1, r++) {
+                    if (r < cbase) continue;
+                    if (r >= cbase + CAND) break;
+                    s_cand[r - cbase] = w * 32 + __builtin_ctz(m);
+                }
+                __syncthreads();
+                const int nc = min(CAND, total - cbase);
+                for (int j0 = 0; j0 < nc; j0 += FCAP) {
+                    const int n = min(FCAP, nc - j0);
+#ifdef NR_FWD_TIMING
+                    const unsigned long long ts0_ = clock64();
+#endif
+                    // records by threads 0 .. n-1 with quarter rows 0-3 of the masks, rows 4-7 by
+                    // threads FCAP .. FCAP + n - 1
+                    if (t < n) {
+                        const float* c = frb + s_cand[j0 + t] * rs;
+                        stage_face<FCAP, CULL, false>(s_face, nullptr, t, c, s_cand[j0 + t], nullptr, false);
+                        reinterpret_cast<uint32_t*>(s_q)[2 * t] = face_quarter_mask<CULL>(c, s_ext4, 0);
+                    } else if (t >= FCAP && t - FCAP < n) {
+                        reinterpret_cast<uint32_t*>(s_q)[2 * (t - FCAP) + 1] =
+                            face_quarter_mask<CULL>(frb + s_cand[j0 + t - FCAP] * rs, s_ext4, 4);
+                    }
+                    if (t == 0) s_next = 0;
+                    __syncthreads();
+#ifdef NR_FWD_TIMING
+                    t_stage += clock64() - ts0_;
+#endif
+                    {  // quarter lengths: wave w counts quarters 4 w .. 4 w + 3 over the staged faces
+                        int cq[4] = {0, 0, 0, 0};
+                        for (int c0 = 0; c0 < n; c0 += 64) {
+                            const uint64_t m = c0 + lane < n ? s_q[c0 + lane] : 0ull;
+#pragma unroll
+                            for (int i = 0; i < 4; i++) cq[i] += __popcll(__ballot((m >> (4 * wid + i)) & 1ull));
+                        }
+                        if (lane < 4) s_qc[4 * wid + lane] = lane == 0 ? cq[0] : lane == 1 ? cq[1] : lane == 2 ? cq[2] : cq[3];
+                    }
+                    __syncthreads();
+                    if (wid == 0) {  // longest first (ties by index): lane q's rank among the 64
+                        const int mc = s_qc[lane];
+                        int rank = 0;
+                        for (int j = 0; j < 64; j++) {
+                            const int oc = s_qc[j];
+                            rank += (oc > mc || (oc == mc && j < lane)) ? 1 : 0;
+                        }
+                        s_qord[rank] = lane;
+                    }
+                    __syncthreads();
+                    for (;;) {
+                        int k = 0;
+                        if (lane == 0) k = atomicAdd(&s_next, 1);
+                        k = __builtin_amdgcn_readfirstlane(k);
+                        if (k >= 64) break;
+                        const int q = s_qord[k];
+                        if (s_qc[q] == 0) break;  // (longest first: the rest are empty too)
+                        const int px = (q & 7) * 4 + (lane & 3), py = (q >> 3) * 4 + ((lane >> 2) & 3);
+                        const bool on = lane < 16;
+                        const int pix = py * COARSE + px;
+                        float dm = on ? s_dm[pix] : -INFINITY;  // lanes 16-63: no pixel (and no share of the wave's depth maximum)
+                        int best = on ? s_best[pix] : -1;
+                        const float xq = pix_center_div(bx0 + px, S), yq = pix_center_div(by0 + py, S);
+                        walk_block<FCAP, false, true, uint64_t, true>(s_face, s_q, q, n, lane, xq, yq, near, far, delta,
+                                                                      dm, best);
+                        if (on) {
+                            s_dm[pix] = dm;
+                            s_best[pix] = best;
+                        }
+                    }
+#ifdef NR_FWD_TIMING
+                    const unsigned long long tw0_ = clock64();
+#endif
+                    __syncthreads();
+#ifdef NR_FWD_TIMING
+                    t_wait += clock64() - tw0_;
+#endif
+                }
+            }
+            wbase += NTF;
+            if (wbase >= g.nwords) break;
+            bits = (wbase + t < g.nwords) ? words[wbase + t] : 0u;
+            off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
+        }
+        // thread t: pixel (t & 31, t >> 5) of the bin
+        const int fbest = s_best[t];
+        {
+            const int px = bx0 + (t & 31), py = by0 + (t >> 5);
+            if (px < S && py < S && (ncand > 0 || !fim_sparse)) fimb[(int)__umul24(py, S) + px] = fbest;
+        }
+        if (SHADE && ncand > 0) {
+            int* s_fim = reinterpret_cast<int*>(s_raw);
+            __syncthreads();
+            s_fim[t] = fbest;
         }
     } else {
         // static blocks: wave w walks its NSUB blocks; the per-pixel state stays in registers over

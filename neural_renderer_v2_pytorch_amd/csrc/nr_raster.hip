@@ -261,7 +261,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         const int rs = vertices ? FACE_REC : 9;
         g_last_fwd.store(LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
                                         (fuse && ntf == 256 && (sh.C == MAXC || sh.draw == static_draw(4)) ? NR_LAUNCH_STATIC_CHANNELS : 0) |
-                                        (ordered ? NR_LAUNCH_DEEP_FIRST : 0) | (side ? NR_LAUNCH_SPLIT : 0)});
+                                        (ordered ? NR_LAUNCH_DEEP_FIRST : 0) | (side ? NR_LAUNCH_SPLIT : 0) |
+                                        (ordered && !side && ntf == 1024 ? NR_LAUNCH_DEALT_QUARTERS : 0)});
         if (side) {
             // fork: the side stream waits for the setup and the order; join: the caller's stream waits
             // for the side stream's launch
@@ -288,7 +289,10 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             if (e) return e;
             if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess)
                 return check_launch("hipEventRecord");
-        } else if (fuse && ntf == 1024)
+        } else if (fuse && ntf == 1024 && ordered)  // deep bins, not split (e.g. one item): dealt quarters
+            hipLaunchKernelGGL((k_raster_fwd<1024, true, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
+                               bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
+        else if (fuse && ntf == 1024)
             hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
@@ -303,6 +307,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         else if (ntf == 256)
             hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
                                F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
+        else if (ordered)
+            hipLaunchKernelGGL((k_raster_fwd<1024, false, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
+                               bbox, mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
         else
             hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);

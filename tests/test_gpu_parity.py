@@ -333,9 +333,10 @@ def test_face_index_dense_snapped_soup(oracle_mod, dev, S, F, seed):
 @pytest.mark.parametrize("zlevels", [0, 3])
 def test_face_index_deep_stack_depth_cull(oracle_mod, dev, zlevels):
     """Bins of 1000+ small faces at random depths (zlevels > 0: only that many distinct depths, so
-    many faces tie within depth_min_delta): the deep variant's deep-first order, its empty-bin skip and
-    its wave-level depth cull (k_raster_fwd walk_block<..., ZCULL>, bins of >= 512 candidates) drop
-    faces behind every pixel of a wave in the ballot; bit-exact against the brute-force oracle."""
+    many faces tie within depth_min_delta): the deep variant's deep-first order, its empty-bin skip,
+    its dealt 4x4 quarters (per-pixel state in LDS across the staging rounds) and its wave-level depth
+    cull (k_raster_fwd walk_block<..., ZCULL>, bins of >= 512 candidates) drop faces behind every
+    pixel of a wave in the ballot; bit-exact against the brute-force oracle."""
     r = np.random.RandomState(7 + zlevels)
     S, F, B = 64, 4000, 2
     cx = r.uniform(-0.9, 0.9, size=(B, F, 1))
@@ -355,7 +356,8 @@ def test_face_index_deep_stack_depth_cull(oracle_mod, dev, zlevels):
     hp.draw_rgb = False
     _, fim = nrr.rasterize_core(verts, faces, nr.RasterizeParam(), hp, return_face_index=True)
     ntf, flags = _lib.last_launch("k_raster_fwd")
-    assert ntf == 1024 and flags & _lib.NR_LAUNCH_DEEP_FIRST, (ntf, flags)
+    # (not split, B % 8 != 0: the deep bins' quarters dealt to the waves)
+    assert ntf == 1024 and flags & _lib.NR_LAUNCH_DEEP_FIRST and flags & _lib.NR_LAUNCH_DEALT_QUARTERS, (ntf, flags)
     assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
     assert (ref[1] >= 0).any() and (ref[1] < 0).any()
 

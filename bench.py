@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 --pmc passes that measure the roofline's HBM traffic and VALU share")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled pass (internal)
+    p.add_argument("--count-child", action="store_true", help=argparse.SUPPRESS)  # face-test counts (internal)
+    p.add_argument("--no-count", action="store_true", help="skip the face-test count (counter-build child)")
     return p.parse_args()
 
 
@@ -228,6 +230,12 @@ def kernel_bytes(w, args, measured=None):
         if rgb and "k_tex_out" not in measured and "k_vertex_grad" in measured:
             # the texture-gradient output carried by k_vertex_grad's blocks (small enough textures)
             k["k_vertex_grad"] += k.pop("k_tex_out")
+    # shared texture windows (NrRasterArgs.face_hot, the car): k_hot_reduce, timed with k_raster_bwd,
+    # reads the 32 private copies of each window (16 texels x 16 B) and adds 48 values into the
+    # texture gradient; the backward's flushes write the copies (counted as its texture-gradient bytes)
+    nh = w.get("num_hot", 0)
+    if nh:
+        k["k_raster_bwd"] += 32 * nh * 256 + nh * 48 * 4 * 2
     total = B * (8 * S * S + 8 * C * s * s + 36 * V) + 24 * F + (2 * T if T else 0)
     return k, total
 
@@ -390,6 +398,65 @@ def pmc_passes(args, timeout_s=240):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def count_child(args):
+    """One forward of the workload through the counter build (bench.py --count-child, NR_LIB_PATH =
+    _lib/libnr_raster_count.so): prints the forward's face-test counters (nr_count_read) as JSON."""
+    import ctypes
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    w = workload(args, 0, dev)
+    from neural_renderer_v2_pytorch_amd import _lib
+    from neural_renderer_v2_pytorch_amd.rasterize import rasterize_core
+    L = _lib.lib()
+    L.nr_count_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    out = (ctypes.c_ulonglong * 4)()
+    step(w)  # warm-up (caches, layouts)
+    torch.cuda.synchronize()
+    _lib.check(L.nr_count_read(out, 1), "nr_count_read")
+    with torch.no_grad():
+        rasterize_core(w["proj"], w["faces"], w["params"](), w["hp"])
+    torch.cuda.synchronize()
+    _lib.check(L.nr_count_read(out, 1), "nr_count_read")
+    print(json.dumps({"tests": out[0], "walked": out[1], "commits": out[2], "walks": out[3]}), flush=True)
+
+
+def face_test_counts(child_args, timeout_s=180):
+    """The forward's face tests, counted by the diagnostic build of the same kernels (-DNR_COUNT_TESTS,
+    built by __graft_entry__.build beside the product library) over one forward of the workload in a
+    child process.  Returns (counts or None, note)."""
+    import subprocess
+    lib = os.path.join(ROOT, "neural_renderer_v2_pytorch_amd", "_lib", "libnr_raster_count.so")
+    if not os.path.exists(lib):
+        return None, "counter build %s missing" % lib
+    try:
+        p = subprocess.run(child_args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout_s, cwd=ROOT,
+                           env=dict(os.environ, NR_LIB_PATH=lib))
+        if p.returncode != 0:
+            return None, "count child exited %d: %s" % (p.returncode, p.stderr.decode(errors="replace")[-300:])
+        return json.loads(p.stdout.decode().strip().splitlines()[-1]), "counter build (-DNR_COUNT_TESTS), one forward"
+    except Exception as e:  # a failed count must not lose the bench line
+        return None, "count child failed: %r" % (e,)
+
+
+def face_test_rate(counts, note, B, S, F, fwd_ms):
+    """SURVEY 8d's secondary bound in its own unit: the (pixel, face) pass tests the forward's walks
+    evaluate per internal pixel and per second of the forward kernel, beside the reference's brute
+    force (B S^2 F tests per call, rasterize_cuda_kernel.cu:82-149) over the same time."""
+    px = B * S * S
+    res = {"source": note, "internal_px": px, "brute_force_tests": px * F}
+    if counts is None:
+        return res
+    t = fwd_ms * 1e-3
+    res.update(tests=counts["tests"], tests_per_px=round(counts["tests"] / px, 3),
+               gtests_per_s=round(counts["tests"] / t / 1e9, 1),
+               brute_force_equivalent_gtests_per_s=round(px * F / t / 1e9, 1),
+               tests_vs_brute_force=round(counts["tests"] / (px * F), 6),
+               faces_walked_per_walk=round(counts["walked"] / max(counts["walks"], 1), 3),
+               commit_batches_per_walk=round(counts["commits"] / max(counts["walks"], 1), 3),
+               fwd_ms=round(fwd_ms, 5))
+    return res
+
+
 def pmc_child(args):
     """One profiled pass (bench.py --pmc-child under rocprofv3): the workload's steps, then the
     calibration stream of known byte count."""
@@ -407,6 +474,8 @@ def main():
     args = parse()
     if args.pmc_child:
         return pmc_child(args)
+    if args.count_child:
+        return count_child(args)
     if args.gpus < 1:
         sys.stderr.write("bench.py: --gpus must be >= 1\n")
         sys.exit(2)
@@ -539,6 +608,13 @@ def main():
         valu_busy = pmc.get("valu_busy", {}).get(dominant)
         valu_insts = pmc.get("valu_insts", {}).get(dominant)
         wait_share = pmc.get("wait_any_share", {}).get(dominant)
+    # the forward's face-test rate (SURVEY 8d's secondary bound), rank 0 at N = 1 like the PMC passes
+    ftr = None
+    if world == 1 and rank == 0 and not args.no_count and "k_raster_fwd" in kms:
+        counts, note = face_test_counts([sys.executable, os.path.join(ROOT, "bench.py"), "--count-child",
+                                         "--batch", str(args.batch), "--image-size", str(args.image_size),
+                                         "--level", str(args.level), "--mode", args.mode])
+        ftr = face_test_rate(counts, note, args.batch, 2 * args.image_size, w["F"], kms["k_raster_fwd"])
     hbm_frac = achieved / HBM_PEAK_GBS
     valu = None
     if valu_insts is not None:
@@ -590,6 +666,11 @@ def main():
                 "valu_busy": round(pmc.get("valu_busy", {}).get(k, 0.0), 4),
                 "wait_share": round(pmc.get("wait_any_share", {}).get(k, 0.0), 4)} for k in pmc["hbm_bytes_per_launch"]},
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
+        # the forward's compute side in the contract's own unit: face tests per internal pixel and per
+        # second (counter build), beside the brute force's B S^2 F
+        "fwd_face_tests_per_px": None if ftr is None else ftr.get("tests_per_px"),
+        "fwd_gtests_per_s": None if ftr is None else ftr.get("gtests_per_s"),
+        "face_test_rate": ftr,
         "step_roofline_frac": round(total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
     }
     if graph_ms is not None:

@@ -56,8 +56,8 @@ NR_API int nr_version(void);
 /* sizeof(NrRasterArgs), for bindings to check their mirror of the struct */
 NR_API size_t nr_raster_args_size(void);
 
-/* ABI version of this header: 5 (NrRasterArgs.face_index_sparse; 4: nr_last_launch; 3: workspace_zeroed of
- * nr_rasterize_backward).
+/* ABI version of this header: 6 (NrRasterArgs.face_hot / num_hot / hot_acc, nr_hot_acc_bytes; 5:
+ * NrRasterArgs.face_index_sparse; 4: nr_last_launch; 3: workspace_zeroed of nr_rasterize_backward).
  * Bindings check it, and nr_raster_args_size(), before the first call. */
 #define NR_ABI_VERSION 6
 
@@ -288,6 +288,17 @@ enum { NR_LAUNCH_FUSED_SHADE = 1, NR_LAUNCH_STATIC_CHANNELS = 2, NR_LAUNCH_TWO_P
        NR_LAUNCH_HOT_WINDOWS = 32 /* k_raster_bwd: shared texture windows into private copies (face_hot) */,
        NR_LAUNCH_DEALT_QUARTERS = 64 /* k_raster_fwd: deep bins' 4x4 quarters dealt to the waves (not split) */ };
 NR_API int nr_last_launch(const char* kernel, int* block_threads, int* flags);
+
+#ifdef NR_COUNT_TESTS
+/* Face-test counters, in the diagnostic build compiled with -DNR_COUNT_TESTS only
+ * (_lib/libnr_raster_count.so, bench.py's face-test rate; SURVEY 8d's secondary bound, the reference's
+ * brute force doing B*S^2*F tests per call, rasterize_cuda_kernel.cu:82-149).  Since the last reset,
+ * out[0] = (pixel, face) pass tests the forward's walks evaluated (64 per face a wave walks over an 8x8
+ * block, 16 over a 4x4 quarter), out[1] = faces walked (wave level), out[2] = deferred commit batches
+ * (the division chain, run by a whole wave), out[3] = walks (8x8 blocks or quarters walked).  reset != 0
+ * zeroes them after the read (device-wide counters: call with the device idle). */
+NR_API int nr_count_read(unsigned long long* out4, int reset);
+#endif
 
 #ifdef __cplusplus
 }

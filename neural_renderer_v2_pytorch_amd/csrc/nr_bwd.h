@@ -220,6 +220,9 @@ struct BwdPix {
 // HOT: the shared-window flush (BwdArgs.face_hot) compiled in; its instantiations run only when the
 // caller passes face_hot (its per-face id load and address select cost the headline's backward 4 %,
 // 0.194 -> 0.202 ms, when compiled into the plain instantiation, gpurun_out/nh)
+#ifdef NR_ABL_S1LOAD
+__device__ float4* g_abl_prod;  // timing builds only: the per-pixel product planes (zeroed)
+#endif
 template <int FEAT, int NPX, int CC = 0, bool HOT = false>
 __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((FEAT & 1) ? 3 : (NPX == 1 ? 6 : 4), 8))) void k_raster_bwd(BwdArgs a, Geom g, Shade sh_in) {
     constexpr bool LIT = (FEAT & 1) != 0, BG = (FEAT & 2) != 0, SILO = (FEAT & 4) != 0;
@@ -375,6 +378,45 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             I2[k][0] = 1.f;
             continue;
         }
+#if defined(NR_ABL_S1ZERO) || defined(NR_ABL_S1LOAD)
+        // timing builds only (the bound of a backward that reads its per-pixel products instead of
+        // recomputing them; values are placeholders, not gradients): S1ZERO recomputes nothing, S1LOAD
+        // loads 48 B per foreground pixel from a lane-ordered buffer (3 coalesced float4 planes)
+        {
+            float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0, v2 = v0;
+#ifdef NR_ABL_S1LOAD
+            const size_t np = (size_t)gridDim.x * gridDim.y * blockDim.x * NPX;
+            const size_t pi = (((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + t) * NPX + k;
+            v0 = g_abl_prod[pi];
+            v1 = g_abl_prod[np + pi];
+            v2 = g_abl_prod[2 * np + pi];
+#endif
+            const float fh = (float)(q.fi & 255) * (1.f / 255.f);
+            q.w[0] = 0.3f + v0.x;
+            q.w[1] = 0.3f + v0.y;
+            q.w[2] = 0.4f + v0.z;
+            I2[k][0] = fh + v0.w;
+            I2[k][1] = 1.f - fh + v1.x;
+            I2[k][2] = 0.5f * fh + v1.y;
+            I2[k][3] = 1.f;
+            I2[k][4] = 2.f + fh + v1.z;
+            q.ay = 0.5f + v1.w;
+            q.by = 0.5f + v2.x;
+            q.ax = 0.25f + v2.y;
+            q.bx = 0.75f + v2.z;
+            q.grgb[0] = G[0];
+            q.grgb[1] = G[1];
+            q.grgb[2] = G[2];
+#pragma unroll
+            for (int j = 0; j < 3; j++) q.gz[j] = G[MAXC - 1] * 0.01f * q.w[j] + v2.w;
+            if (want_tex) {
+                q.wx = (q.fi % 72) * 4;
+                q.wy = (q.fi / 72) * 4;
+                q.pos = 5;
+            }
+            continue;
+        }
+#endif
         Face f = load_face_rec(frb + q.fi * FACE_REC);
         // the texture record with the face record: one round trip for both (unconditional, so that
         // no branch join needs its value: without rgb it reads the face record's first 32 bytes)
@@ -901,6 +943,20 @@ void launch_bwd_v(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, c
 // passes face_hot for no other (nr_rasterize_backward)
 template <int FEAT>
 void launch_bwd(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, const Shade& sh) {
+#ifdef NR_ABL_S1LOAD
+    {  // timing builds only: a zeroed buffer of 3 float4 planes, one entry per (thread, pixel) of the grid
+        static float4* buf = nullptr;
+        static size_t have = 0;
+        const size_t need = (size_t)grid.x * grid.y * NT * 2 * 3 * sizeof(float4);
+        if (need > have) {
+            if (buf) (void)hipFree(buf);
+            if (hipMalloc(&buf, need) != hipSuccess || hipMemset(buf, 0, need) != hipSuccess ||
+                hipMemcpyToSymbol(HIP_SYMBOL(g_abl_prod), &buf, sizeof(buf)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+                abort();
+            have = need;
+        }
+    }
+#endif
     if constexpr (FEAT == 0) {
         if (ba.face_hot) {
             launch_bwd_v<FEAT, true>(grid, st, ba, g, sh);

@@ -467,6 +467,10 @@ constexpr int ZCULL_MIN = 512;  // candidates of a bin (first bin-mask round)
 // one wave's walk of the n staged faces over its 8x8 block u of the bin (pixel (xp, yp) per lane): the
 // ballot takes the staged faces whose block mask (face_block_mask: bbox, and with CULL the edge cull)
 // has bit u, then the per-face test runs in ascending order
+#ifdef NR_COUNT_TESTS
+// diagnostic build: face tests, faces walked, commit batches, walks (nr_count_read)
+__device__ unsigned long long g_fwd_count[4];
+#endif
 template <int FST, bool SLOT, bool ZCULL = false, typename MT = uint16_t, bool Q16 = false>
 __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, const MT* __restrict__ s_bm, int u,
                                            int n, int lane, float xp, float yp, float near, float far, float delta,
@@ -482,6 +486,9 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, co
     // version cost +4 us each (same-box A/Bs, gpurun_out/o4-o9).
     float zmax = 0.f;
     bool dirty = true;  // (wave-uniform) a commit may have lowered a depth since zmax was taken
+#ifdef NR_COUNT_TESTS
+    unsigned long long cnt_walked = 0, cnt_commits = 0;
+#endif
     for (int c0 = 0; c0 < n; c0 += 64) {
         if (ZCULL && dirty && (c0 & NR_ZREFRESH) == 0) {
             zmax = wave_max(depth_min);
@@ -496,6 +503,9 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, co
         for (unsigned long long m = __ballot(hit); m; m &= m - 1) {
             const int slot = c0 + __builtin_ctzll(m);
             const float4* e = s_face + slot;
+#ifdef NR_COUNT_TESTS
+            cnt_walked++;
+#endif
             FaceRows<FST> fr;
             fr.load(e);
             // the pass test with its outcome kept as a wave mask: the depth and bbox tests of every lane
@@ -520,6 +530,9 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, co
                 cov = lane_mask_uge(c1 * c2, 0.f) & lane_mask_uge(c3 * c2, 0.f) & pre;
             }
             if (cov & occ) {  // commit first where this face would queue behind a pending one
+#ifdef NR_COUNT_TESTS
+                cnt_commits++;
+#endif
                 if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
                 pend = -1;
                 occ = 0;
@@ -532,6 +545,15 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, co
             occ |= cov;
         }
     }
+#ifdef NR_COUNT_TESTS
+    if (occ) cnt_commits++;
+    if (lane == 0) {
+        atomicAdd(&g_fwd_count[0], cnt_walked * (Q16 ? 16ull : 64ull));
+        atomicAdd(&g_fwd_count[1], cnt_walked);
+        atomicAdd(&g_fwd_count[2], cnt_commits);
+        atomicAdd(&g_fwd_count[3], 1ull);
+    }
+#endif
     if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
 }
 

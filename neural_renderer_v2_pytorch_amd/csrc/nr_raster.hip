@@ -92,8 +92,11 @@ size_t nr_workspace_bytes(int batch_size, int num_faces, int image_size) {
 
 // A side stream per (host thread, device) for the split forward, with its fork / join events; created
 // on first use outside a stream capture (null: no split for this call).  The thread's table releases
-// them when the thread ends (a worker pool's recycled threads do not accumulate streams); the streams
-// are synchronised first, so work still queued on one finishes before it is destroyed.
+// them when the thread ends (a worker pool's recycled threads do not accumulate streams).  No
+// synchronisation there: hipStreamDestroy of a stream with queued work returns at once and releases it
+// when the work is done, and a synchronising call from an exiting thread would invalidate another
+// thread's graph capture in global capture mode; the destroys themselves run in this thread's relaxed
+// capture mode for the same reason.  Errors are ignored (at process exit the runtime may be gone).
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -101,15 +104,18 @@ struct SideStream {
 struct SideStreamTable {
     SideStream tab[64];
     ~SideStreamTable() {
+        bool any = false;
+        for (const SideStream& x : tab) any = any || x.s || x.fork || x.join;
+        if (!any) return;
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        const bool exch = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
         for (SideStream& x : tab) {
-            if (x.s) {
-                (void)hipStreamSynchronize(x.s);
-                (void)hipStreamDestroy(x.s);
-            }
+            if (x.s) (void)hipStreamDestroy(x.s);
             if (x.fork) (void)hipEventDestroy(x.fork);
             if (x.join) (void)hipEventDestroy(x.join);
             x = SideStream{};
         }
+        if (exch) (void)hipThreadExchangeStreamCaptureMode(&mode);
     }
 };
 #ifndef NR_SPLIT_BUCKET
@@ -551,14 +557,17 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
             case 3: launch_bwd<3>(grid, st, ba, g, sh); break;
             default: launch_bwd<4>(grid, st, ba, g, sh); break;
         }
-    }
-    e = check_launch("k_raster_bwd");
-    if (e) return e;
-    if (hot) {  // before the texture-gradient output (k_vertex_grad / k_tex_out) reads the accumulator
-        hipLaunchKernelGGL(k_hot_reduce, dim3((unsigned)a->num_hot), dim3(64), 0, st, a->hot_acc, a->num_hot, g4,
-                           a->tex_width, a->tex_height);
-        e = check_launch("k_hot_reduce");
+        e = check_launch("k_raster_bwd");
         if (e) return e;
+        // the shared windows' private copies, summed (timed with k_raster_bwd, whose window flushes they
+        // complete; bench.py counts their bytes there), before the texture-gradient output (k_vertex_grad
+        // / k_tex_out) reads the accumulator
+        if (hot) {
+            hipLaunchKernelGGL(k_hot_reduce, dim3((unsigned)a->num_hot), dim3(64), 0, st, a->hot_acc, a->num_hot, g4,
+                               a->tex_width, a->tex_height);
+            e = check_launch("k_hot_reduce");
+            if (e) return e;
+        }
     }
     const long long nv = (long long)a->batch_size * a->num_vertices;
     if (lit && nv > 0) {
@@ -779,6 +788,20 @@ int nr_profile_enable(int on) {
     g_prof = on != 0;
     return NR_OK;
 }
+
+#ifdef NR_COUNT_TESTS
+int nr_count_read(unsigned long long* out4, int reset) {
+    if (!out4) return fail(NR_ERR_ARGS, "null argument");
+    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_fwd_count), 4 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(NR_ERR_LAUNCH, "nr_count_read: hipMemcpyFromSymbol failed");
+    if (reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_count), z, sizeof(z)) != hipSuccess)
+            return fail(NR_ERR_LAUNCH, "nr_count_read: hipMemcpyToSymbol failed");
+    }
+    return NR_OK;
+}
+#endif
 
 int nr_profile_read(const char* kernel, float* ms) {
     if (!kernel || !ms) return fail(NR_ERR_ARGS, "null argument");

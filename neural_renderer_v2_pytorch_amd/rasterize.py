@@ -221,6 +221,8 @@ def _face_hot(ft, vt_src, dev):
     hit = _hot_cache.get(key)
     if hit is not None:
         return hit[0], hit[1]
+    if vt_src.is_cuda and torch.cuda.is_current_stream_capturing():
+        return None, 0  # the grouping needs a host copy; the plain flush is exact without it
     import numpy as np
     if _HOT_MIN_FACES <= 0 or ft.shape[0] == 0:
         res = (None, 0)
@@ -473,9 +475,14 @@ class Rasterize(torch.autograd.Function):
         grads = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         uv_items = (1 if vt_bstride == 0 else B) if rgb else 0
         nl = light_recs.shape[0] if light_recs is not None else 0
-        # shared texture windows (a texture and texture coordinates shared by the batch, texture gradient wanted)
+        # shared texture windows (a texture and texture coordinates shared by the batch, texture gradient
+        # wanted).  Only for a fixed texture-coordinate table: the grouping is computed on the host from
+        # the table's values and cached per (storage, version), so a trainable vt (updated in place every
+        # step, or inside a captured graph whose replays never re-run the host code) would keep a stale
+        # grouping and send diverged windows' sums to one slot.  A cache miss during stream capture (its
+        # host copy would raise) also goes without.
         face_hot, num_hot = None, 0
-        if rgb and ctx.needs_input_grad[1] and cfg.tex_shared and vt_bstride == 0:
+        if rgb and ctx.needs_input_grad[1] and not ctx.needs_input_grad[2] and cfg.tex_shared and vt_bstride == 0:
             face_hot, num_hot = _face_hot(faces_textures, vertices_textures[0] if vertices_textures.ndim == 3
                                           else vertices_textures, dev)
         lay = _layout(L, cfg, uv_items, _HALO_CACHE and grads, _BWD_PREZERO and grads,

@@ -1339,3 +1339,40 @@ def test_shared_texture_windows_vs_oracle(oracle_mod, dev):
     _, _, rgv, rgt = oracle_batch(oracle_mod, proj, f, g, s, torch.as_tensor(tex), vt, ft)
     close_grads(gt, rgt, "shared windows: grad textures vs oracle")
     close_grads(gv, rgv, "shared windows: grad vertices vs oracle")
+
+
+@pytest.mark.gpu
+def test_shared_texture_windows_off_for_trainable_vt(oracle_mod, dev):
+    """The shared-window grouping (face_hot) is computed on the host from the texture-coordinate
+    table's values, so it is used only for a fixed table: with vertices_textures requiring a gradient
+    (an optimiser moves it in place between steps, which a grouping cached per (storage, version), or
+    captured in a graph, would not see) the backward takes the plain window flush.  Two steps with the
+    table edited in place between them (under no_grad, as an optimiser step does): no hot-window
+    launch either time, and the second step's texture gradient matches the oracle at the edited table
+    (three of the formerly identical triples now diverge)."""
+    B, s = 4, 64
+    proj, f = _ico_batch(3, B, dev)
+    faces = torch.as_tensor(f, device=dev)
+    vt0 = np.array([[[0, p], [0, p + 1], [1, p + 1]] for p in (0, 2, 4)], np.float32).reshape(-1, 2)
+    ft = np.stack([np.arange(3) + 3 * (i % 3) for i in range(f.shape[0])]).astype(np.int32)
+    tex = np.random.RandomState(81).uniform(0, 1, (3, 8, 8)).astype(np.float32)
+    g = torch.as_tensor(np.random.RandomState(82).normal(size=(B, 5, s, s)).astype(np.float32), device=dev)
+    vtp = torch.as_tensor(vt0, device=dev).requires_grad_(True)
+    for step in range(2):
+        v = proj.detach().to(dev).requires_grad_(True)
+        t = torch.as_tensor(tex, device=dev).requires_grad_(True)
+        params = nr.RasterizeParam(vertices_textures=vtp[None].expand(B, -1, -1),
+                                   faces_textures=torch.as_tensor(ft, device=dev),
+                                   textures=t[None].expand(B, -1, -1, -1))
+        img = nrr.rasterize_core(v, faces, params, nr.RasterizeHyperparam(image_size=s))
+        img.backward(g)
+        assert not _lib.last_launch("k_raster_bwd")[1] & _lib.NR_LAUNCH_HOT_WINDOWS
+        if step == 0:
+            with torch.no_grad():
+                vtp[3:6] += torch.tensor([[0.5, 0.25], [0.75, 0.5], [1.25, 0.5]], device=dev)
+            vtp.grad = None
+    vt1 = vtp.detach().cpu().numpy()
+    assert not np.array_equal(vt1, vt0)
+    _, _, rgv, rgt = oracle_batch(oracle_mod, proj, f, g, s, torch.as_tensor(tex), vt1, ft)
+    close_grads(t.grad, rgt, "trainable vt, edited table: grad textures vs oracle")
+    close_grads(v.grad, rgv, "trainable vt, edited table: grad vertices vs oracle")

@@ -91,8 +91,16 @@ def test_synthetic_meshes():
 def test_library_exports_every_header_symbol():
     """The C-ABI library loads and exports exactly what include/nr_raster.h declares."""
     header = open(os.path.join(ROOT, "include", "nr_raster.h")).read()
-    declared = set(re.findall(r"^\s*(?:NR_API\s+)?(?:const\s+)?\w+\s*\*?\s*(nr_\w+)\s*\(", header, re.M))
+    # the diagnostic build's counters (#ifdef NR_COUNT_TESTS) are declared for that build only
+    diag = re.findall(r"^#ifdef NR_COUNT_TESTS\n(.*?)^#endif", header, re.M | re.S)
+    header = re.sub(r"^#ifdef NR_COUNT_TESTS\n.*?^#endif", "", header, flags=re.M | re.S)
+    decl = r"^\s*(?:NR_API\s+)?(?:const\s+)?\w+\s*\*?\s*(nr_\w+)\s*\("
+    declared = set(re.findall(decl, header, re.M))
     assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    assert set(re.findall(decl, "".join(diag), re.M)) == {"nr_count_read"}
+    count_lib = os.path.join(_lib.LIB_DIR, "libnr_raster_count.so")
+    assert hasattr(ctypes.CDLL(count_lib), "nr_count_read")
+    assert not hasattr(ctypes.CDLL(_lib.LIB_PATH), "nr_count_read")
     L = ctypes.CDLL(_lib.LIB_PATH)
     for name in declared:
         assert hasattr(L, name), name

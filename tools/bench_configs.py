@@ -172,7 +172,11 @@ def cfg3_step(dev):
     def step():
         proj.grad = tex.grad = None
         nr.rasterize_rgba(proj, faces, params, nr.RasterizeHyperparam(image_size=s)).backward(g)
-    step.meta = dict(batch=B, image_size=s, C=4, V=int(v.shape[0]), F=int(f.shape[0]), tex_shape=tuple(tex.shape))
+    from neural_renderer_v2_pytorch_amd import rasterize as nrr
+    # the shared texture windows the backward sums in private copies (k_hot_reduce, bytes in bench.kernel_bytes)
+    num_hot = nrr._face_hot(params.faces_textures, params.vertices_textures[0], dev)[1]
+    step.meta = dict(batch=B, image_size=s, C=4, V=int(v.shape[0]), F=int(f.shape[0]), tex_shape=tuple(tex.shape),
+                     num_hot=num_hot)
     return step, f, B, s
 
 
@@ -252,7 +256,7 @@ def roofline(meta, kms, step_ms, step_from):
     HBM roof; and the whole step's bytes B(8S^2 + 8Cs^2 + 36V) + 24F + 2T over the step time."""
     import argparse
     import bench
-    w = dict(C=meta["C"], V=meta["V"], F=meta["F"], tex_shape=meta["tex_shape"])
+    w = dict(C=meta["C"], V=meta["V"], F=meta["F"], tex_shape=meta["tex_shape"], num_hot=meta.get("num_hot", 0))
     args = argparse.Namespace(batch=meta["batch"], image_size=meta["image_size"])
     kb, total = bench.kernel_bytes(w, args, kms)
     per = {}
@@ -302,6 +306,41 @@ def pmc_traffic(name, timeout_s=240):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def config_step(name, dev):
+    """(step, meta) of config `name`."""
+    if name == "cfg2":
+        return cfg2_step(dev)
+    st = {"cfg3": cfg3_step, "cfg5": cfg5_step}[name](dev)[0]
+    return st, st.meta
+
+
+def count_child(name):
+    """One step of config `name` through the counter build (NR_LIB_PATH = _lib/libnr_raster_count.so,
+    set by the parent): prints that step's forward face-test counters (nr_count_read) as JSON."""
+    import ctypes
+    from neural_renderer_v2_pytorch_amd import _lib
+    dev = torch.device("cuda", 0)
+    step, _ = config_step(name, dev)
+    L = _lib.lib()
+    L.nr_count_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    out = (ctypes.c_ulonglong * 4)()
+    step()
+    torch.cuda.synchronize()
+    _lib.check(L.nr_count_read(out, 1), "nr_count_read")
+    step()
+    torch.cuda.synchronize()
+    _lib.check(L.nr_count_read(out, 1), "nr_count_read")
+    print(json.dumps({"tests": out[0], "walked": out[1], "commits": out[2], "walks": out[3]}), flush=True)
+
+
+def face_tests(name, r, meta):
+    """The forward's face-test rate of config `name` (bench.face_test_rate over a counter-build child)."""
+    import bench
+    counts, note = bench.face_test_counts([sys.executable, os.path.abspath(__file__), "--count-child", name])
+    S = meta["image_size"] * 2
+    return bench.face_test_rate(counts, note, meta["batch"], S, meta["F"], r["kernels_ms"]["k_raster_fwd"])
+
+
 def main():
     p = argparse.ArgumentParser()
     # steady state (as bench.py: five warm-up steps left the GPU short of it, profiles/r05_warmup.txt)
@@ -316,12 +355,22 @@ def main():
                    help="add each config's PMC traffic per kernel (two rocprofv3 --pmc passes per config) and its "
                         "ratio to the algorithmic bytes")
     p.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)  # one profiled pass (internal)
+    p.add_argument("--count-child", default=None, help=argparse.SUPPRESS)  # face-test counts (internal)
+    p.add_argument("--no-count", action="store_true", help="skip the face-test counts (counter-build child)")
     a = p.parse_args()
     if a.pmc_child:
         return pmc_child(a.pmc_child)
+    if a.count_child:
+        return count_child(a.count_child)
     dev = torch.device("cuda", 0)
     for name in a.only.split(","):
         r = globals()[name](dev, a)
+        if not a.no_count and "k_raster_fwd" in r.get("kernels_ms", {}):
+            meta = dict(batch=r["batch"], image_size=r["image_size"], F=r["faces"])
+            ftr = face_tests(name, r, meta)
+            r["fwd_face_tests_per_px"] = ftr.get("tests_per_px")
+            r["fwd_gtests_per_s"] = ftr.get("gtests_per_s")
+            r["face_test_rate"] = ftr
         if a.pmc:
             try:
                 tr = pmc_traffic(name)

@@ -243,9 +243,14 @@ def kernel_bytes(w, args, measured=None):
 KERNELS = ["k_tex_pack", "k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
 
 
-def time_kernels(w, n=10):
+def time_kernels(w, n=10, run=4):
     """Per-kernel durations from HIP events the library records on its launch stream around each
-    launch (nr_profile_enable / nr_profile_read), averaged over n fwd+bwd calls."""
+    launch (nr_profile_enable/read; each launch's pair overwrites the previous one's), averaged over n
+    samples.  Each sample is the last of `run` back-to-back steps, so the kernels it times run as in
+    the timed loop, behind other steps' work: a synchronisation before every sampled step leaves the
+    GPU idle for the host's enqueue time, and after such gaps the same kernels measured ~7 % slower
+    (round 6: bwd 0.208 against 0.193 ms by the rocprofv3 trace of a pipelined run on one box; the
+    memory side's power state, tools/warm_probe.py)."""
     import ctypes
     from neural_renderer_v2_pytorch_amd import _lib
     L = _lib.lib()
@@ -253,7 +258,8 @@ def time_kernels(w, n=10):
     acc = {k: [] for k in KERNELS}
     try:
         for _ in range(n):
-            step(w)
+            for _ in range(run):
+                step(w)
             torch.cuda.synchronize()
             for k in KERNELS:
                 ms = ctypes.c_float()
@@ -559,6 +565,21 @@ def main():
         host_single = (time.perf_counter() - t1) / args.steps * 1e3
         torch.cuda.synchronize()
 
+    # the host's own cost of enqueueing one step: with the GPU idle before each step (synchronised), so
+    # that no launch waits for queue space.  host_ms_per_step above is measured inside the timed loop,
+    # where the host runs ahead of the GPU until the runtime's launch queue is full and then waits for
+    # it: it includes that back-pressure and so rises toward the GPU step time on any box (0.21-0.31 ms
+    # on two boxes whose idle-GPU enqueue of the same step took ~0.1 ms, round 6), which is why it is
+    # not the host's cost.
+    host_idle = []
+    for _ in range(10):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step(w)
+        host_idle.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    host_idle_ms = float(np.median(host_idle)) * 1e3
+
     graph_ms = None
     if args.graph_steps > 0:
         images = images.detach()  # release the last eager step's autograd graph before the capture
@@ -610,7 +631,8 @@ def main():
         wait_share = pmc.get("wait_any_share", {}).get(dominant)
     # the forward's face-test rate (SURVEY 8d's secondary bound), rank 0 at N = 1 like the PMC passes
     ftr = None
-    if world == 1 and rank == 0 and not args.no_count and "k_raster_fwd" in kms:
+    # (not under rocprofv3: the child would inherit the profiler's preload, as the PMC passes would)
+    if world == 1 and rank == 0 and not args.no_count and "k_raster_fwd" in kms and not under_profiler():
         counts, note = face_test_counts([sys.executable, os.path.join(ROOT, "bench.py"), "--count-child",
                                          "--batch", str(args.batch), "--image-size", str(args.image_size),
                                          "--level", str(args.level), "--mode", args.mode])
@@ -649,6 +671,7 @@ def main():
                    "global_batch": world * args.batch, "image_size": args.image_size, "faces": w["F"],
                    "channels": w["C"], "parallelism": "batch-sharded dp%d" % world},
         "host_ms_per_step": round(host_elapsed / args.steps * 1e3, 4),
+        "host_ms_per_step_idle_gpu": round(host_idle_ms, 4),
         "host_ms_per_step_autograd_single_thread": round(host_single, 4),
         # achieved / peak / frac are against the HBM roof (the contract's "bound"); the VALU roof beside
         # it, the closer of the two, and what limits the kernel

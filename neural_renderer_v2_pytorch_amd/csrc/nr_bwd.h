@@ -240,8 +240,26 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     }
     constexpr int REC = srec<LIT>();
     __shared__ __attribute__((aligned(16))) float s_raw[bwd_lds<LIT>() / 4];
-    float(*s_I)[HN] = reinterpret_cast<float(*)[HN]>(s_raw);
-    float(*s_G)[HN] = reinterpret_cast<float(*)[HN]>(s_raw + MAXC * HN);
+    // the tile's image and upstream gradient (+ halo) in LDS, (I_c, G_c) interleaved per pixel in three
+    // planes: (I0 G0 I1 G1), (I2 G2 I3 G3), (I4 G4) -- a pixel's ten values are 3 LDS accesses
+    // (ds_read_b128 x 2 + ds_read_b64) instead of 10 dword accesses; unused channels hold 0
+    static_assert(MAXC == 5, "interleaved I/G planes");
+    float4* s_ig01 = reinterpret_cast<float4*>(s_raw);
+    float4* s_ig23 = s_ig01 + HN;
+    float2* s_ig4 = reinterpret_cast<float2*>(s_ig23 + HN);
+    static_assert(HN * (16 + 16 + 8) == BWD_LDS_IG, "I/G planes fill BWD_LDS_IG");
+    auto store_ig = [&](int i, const float* I, const float* G) {
+        s_ig01[i] = make_float4(I[0], G[0], I[1], G[1]);
+        s_ig23[i] = make_float4(I[2], G[2], I[3], G[3]);
+        s_ig4[i] = make_float2(I[4], G[4]);
+    };
+    auto load_ig = [&](int i, float* I, float* G) {
+        const float4 a01 = s_ig01[i], a23 = s_ig23[i];
+        const float2 a4 = s_ig4[i];
+        I[0] = a01.x; G[0] = a01.y; I[1] = a01.z; G[1] = a01.w;
+        I[2] = a23.x; G[2] = a23.y; I[3] = a23.z; G[3] = a23.w;
+        I[4] = a4.x; G[4] = a4.y;
+    };
     const int S = g.S;
     const int C = CC ? CC : sh.C;
     const bool rgb = !SILO && (sh.draw & NR_DRAW_RGB) != 0;
@@ -317,7 +335,11 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         }
     };
     NR_TSTAMP(0);
+#ifndef NR_ABL_NOSTENCIL
     halo_prefetch();  // in flight during step 1
+#else
+    (void)halo_prefetch;
+#endif
 
     // ---- 1. image + upstream gradient (LDS), and the stencil-independent gradient terms ---------
     BwdPix P[NPX];
@@ -547,17 +569,9 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         I2[k][3] = Sl ? 1.f : dep;
         I2[k][4] = dep;
     }
+#ifndef NR_ABL_NOSTENCIL  // timing builds only: no LDS staging, halo or pair terms (placeholder stencil)
 #pragma unroll
-    for (int k = 0; k < NPX; k++) {
-        const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) {
-            if (c < C) {
-                s_I[c][li] = I2[k][c];
-                s_G[c][li] = G2[k][c];
-            }
-        }
-    }
+    for (int k = 0; k < NPX; k++) store_ig((ly0 + 4 * k + 1) * HW_ + (lx + 1), I2[k], G2[k]);
     // halo ring: image and upstream gradient only
     int hy, hx;
     halo_pixel(t, hy, hx);
@@ -568,14 +582,13 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         // each lane t < NHALO moves the halo values it loaded itself (s_hI/s_hG slot t), so its own
         // vmcnt wait is enough: no barrier before the move
         if (t < NHALO) {
-            const int hl = hy * HW_ + hx;
+            float hI[MAXC], hG[MAXC];
 #pragma unroll
             for (int c = 0; c < MAXC; c++) {
-                if (c < C) {
-                    s_I[c][hl] = h_in && h_live ? s_hI[c][t] : 0.f;
-                    s_G[c][hl] = h_in ? (a.aa ? s_hG[c][t] / 4.f : s_hG[c][t]) : 0.f;
-                }
+                hI[c] = c < C && h_in && h_live ? s_hI[c][t] : 0.f;
+                hG[c] = c < C && h_in ? (a.aa ? s_hG[c][t] / 4.f : s_hG[c][t]) : 0.f;
             }
+            store_ig(hy * HW_ + hx, hI, hG);
         }
     } else if (t < NHALO) {
         float hI[MAXC], hG[MAXC];
@@ -589,14 +602,7 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
             shade_pixel(sh, b, hf, ff, fu, hpx, hpy, pix_center(hpx, S), pix_center(hpy, S), S, hI);
             upstream_grad(a, gimb, C, hpy, hpx, S, hG);
         }
-        const int hl = hy * HW_ + hx;
-#pragma unroll
-        for (int c = 0; c < MAXC; c++) {
-            if (c < C) {
-                s_I[c][hl] = hI[c];
-                s_G[c][hl] = hG[c];
-            }
-        }
+        store_ig(hy * HW_ + hx, hI, hG);
     }
     NR_TSTAMP(1);
     __syncthreads();
@@ -612,19 +618,25 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
     float2* s_px = reinterpret_cast<float2*>(s_raw + (BWD_LDS_IG + BWD_LDS_HALO) / 4);  // [HN]: pair (i, i + 1)
     float2* s_py = s_px + HN;                                                            // [HN]: pair (i, i + row)
     static_assert(BWD_LDS_IG + BWD_LDS_HALO + 2 * HN * 8 <= bwd_lds<LIT>(), "pair terms fit the block's LDS");
+    // (the pixel's own I and G are this lane's registers, the values it staged: no LDS read for them)
+    float2 own_px[NPX], own_py[NPX];
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
         const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
-        float I0[MAXC], G0[MAXC], dx[MAXC], dy[MAXC], Gx[MAXC], Gy[MAXC];
+        float I0[MAXC], G0[MAXC], dx[MAXC], dy[MAXC], Gx[MAXC], Gy[MAXC], Ix[MAXC], Iy[MAXC];
+        load_ig(li + 1, Ix, Gx);
+        load_ig(li + HW_, Iy, Gy);
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
             const bool u = c < C;
-            I0[c] = u ? s_I[c][li] : 0.f; G0[c] = u ? s_G[c][li] : 0.f;
-            dx[c] = u ? I0[c] - s_I[c][li + 1] : 0.f; Gx[c] = u ? s_G[c][li + 1] : 0.f;
-            dy[c] = u ? I0[c] - s_I[c][li + HW_] : 0.f; Gy[c] = u ? s_G[c][li + HW_] : 0.f;
+            I0[c] = u ? I2[k][c] : 0.f; G0[c] = u ? G2[k][c] : 0.f;
+            dx[c] = u ? I0[c] - Ix[c] : 0.f; Gx[c] = u ? Gx[c] : 0.f;
+            dy[c] = u ? I0[c] - Iy[c] : 0.f; Gy[c] = u ? Gy[c] : 0.f;
         }
-        s_px[li] = make_float2(diff_dot(dx, Gx, C), diff_dot(dx, G0, C));
-        s_py[li] = make_float2(diff_dot(dy, Gy, C), diff_dot(dy, G0, C));
+        own_px[k] = make_float2(diff_dot(dx, Gx, C), diff_dot(dx, G0, C));
+        own_py[k] = make_float2(diff_dot(dy, Gy, C), diff_dot(dy, G0, C));
+        s_px[li] = own_px[k];
+        s_py[li] = own_py[k];
     }
     {
         // the pairs whose first pixel is a halo pixel: left column rows 1..BH (wave 0), top row
@@ -632,13 +644,15 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         const bool lc = t < BH, tr = t >= 64 && t < 64 + TW;
         if (lc || tr) {
             const int li = lc ? (t + 1) * HW_ : t - 63, lj = lc ? li + 1 : li + HW_;
-            float d[MAXC], Gi[MAXC], Gj[MAXC];
+            float d[MAXC], Gi[MAXC], Gj[MAXC], Ii[MAXC], Ij[MAXC];
+            load_ig(li, Ii, Gi);
+            load_ig(lj, Ij, Gj);
 #pragma unroll
             for (int c = 0; c < MAXC; c++) {
                 const bool u = c < C;
-                d[c] = u ? s_I[c][li] - s_I[c][lj] : 0.f;
-                Gi[c] = u ? s_G[c][li] : 0.f;
-                Gj[c] = u ? s_G[c][lj] : 0.f;
+                d[c] = u ? Ii[c] - Ij[c] : 0.f;
+                Gi[c] = u ? Gi[c] : 0.f;
+                Gj[c] = u ? Gj[c] : 0.f;
             }
             const float2 v = make_float2(diff_dot(d, Gj, C), diff_dot(d, Gi, C));
             if (lc) s_px[li] = v;
@@ -646,6 +660,10 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         }
     }
     __syncthreads();
+#else
+    float gF[NPX][9];
+    (void)h_live;
+#endif
 #pragma unroll
     for (int k = 0; k < NPX; k++) {
         BwdPix& q = P[k];
@@ -653,9 +671,13 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
         for (int j = 0; j < 9; j++) gF[k][j] = 0.f;
         if (q.fi < 0) continue;
         const int py = ty0 + ly0 + 4 * k;
+#ifndef NR_ABL_NOSTENCIL
         const int li = (ly0 + 4 * k + 1) * HW_ + (lx + 1);
-        const float gx = stencil_pair(a, s_px[li], s_px[li - 1], px, S);
-        const float gy = stencil_pair(a, s_py[li], s_py[li - HW_], py, S);
+        const float gx = stencil_pair(a, own_px[k], s_px[li - 1], px, S);
+        const float gy = stencil_pair(a, own_py[k], s_py[li - HW_], py, S);
+#else
+        const float gx = (I2[k][0] - I2[k][1]) * G2[k][0] * 7.f, gy = (I2[k][2] - I2[k][MAXC - 1]) * G2[k][1] * 5.f;
+#endif
         if (wlate && (gx != 0.f || gy != 0.f)) {
             // silhouettes only: the stencil is zero away from silhouette edges, so only these pixels
             // fetch their face and weights (the same computation as in step 1)

@@ -148,7 +148,13 @@ __device__ __forceinline__ int range_hi(int p) { return p >> 16; }
 // shortcut (rcp_nr(z_k), rcp_nr(z_k + 1e-10)) and the operand-range flags that allow it.  Faces
 // handed over by the caller (face_index_map_forward_safe, compute_weight_map) are 9 floats and
 // always take the plain IEEE divisions (flags = 0).
+#ifdef NR_REC48
+// timing builds only: 48-B records (corners and flags; the six reciprocals recomputed where a record is
+// loaded), the record DESIGN.md section 9 item 5 modelled
+constexpr int FACE_REC = 12;
+#else
 constexpr int FACE_REC = 16;
+#endif
 constexpr int FACE_FAST_XYZ = 1;  // x, y in {0} u [2^-20, 2^20], |z| in [2^-20, 2^20]
 constexpr int FACE_FAST_ZQ = 2;   // |z + 1e-10| in [2^-20, 2^20]
 constexpr int FACE_ZQ_EQ = 4;     // z + 1e-10 == z for every corner (|z| >= ~2^-6): w / (z + 1e-10) == w / z
@@ -168,6 +174,21 @@ __device__ __forceinline__ Face load_face(const float* __restrict__ fr) {
     return f;
 }
 
+#ifdef NR_REC48
+__device__ __forceinline__ float face_rcp(float x);
+__device__ __forceinline__ Face load_face_rec(const float* __restrict__ fr) {
+    const float4* p = reinterpret_cast<const float4*>(fr);
+    const float4 a = p[0], b = p[1], c = p[2];
+    Face f;
+    f.x0 = a.x; f.y0 = a.y; f.z0 = a.z;
+    f.x1 = a.w; f.y1 = b.x; f.z1 = b.y;
+    f.x2 = b.z; f.y2 = b.w; f.z2 = c.x;
+    f.rz0 = face_rcp(f.z0); f.rz1 = face_rcp(f.z1); f.rz2 = face_rcp(f.z2);
+    f.rq0 = face_rcp(f.z0 + 1e-10f); f.rq1 = face_rcp(f.z1 + 1e-10f); f.rq2 = face_rcp(f.z2 + 1e-10f);
+    f.flags = __float_as_int(c.y);
+    return f;
+}
+#else
 __device__ __forceinline__ Face load_face_rec(const float* __restrict__ fr) {
     const float4* p = reinterpret_cast<const float4*>(fr);
     const float4 a = p[0], b = p[1], c = p[2], d = p[3];
@@ -180,6 +201,7 @@ __device__ __forceinline__ Face load_face_rec(const float* __restrict__ fr) {
     f.flags = __float_as_int(d.w);
     return f;
 }
+#endif
 
 __device__ __forceinline__ Face empty_face() {
     Face f = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};

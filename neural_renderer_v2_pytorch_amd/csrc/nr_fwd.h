@@ -36,6 +36,9 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
         b = (L & 7) + 8 * (j / gridDim.x);
         grp = j % gridDim.x;
     } else {
+        // (round 6: the (item, group) tasks in 8 contiguous chunks, one per XCD, so that neighbouring
+        // face groups' mask pieces would meet in one L2 for other batch sizes too: the torus and teapot
+        // setups measured the same, 16.2-16.4 / 10.6-10.7 us, gpurun_out/chunk; not kept)
         b = blockIdx.y;
         grp = blockIdx.x;
     }
@@ -73,9 +76,13 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                 float4* rec = reinterpret_cast<float4*>(s_frec + t * FACE_REC);
                 rec[0] = make_float4(c[0], c[1], c[2], c[3]);
                 rec[1] = make_float4(c[4], c[5], c[6], c[7]);
+#ifdef NR_REC48
+                rec[2] = make_float4(c[8], __int_as_float(flags), 0.f, 0.f);
+#else
                 rec[2] = make_float4(c[8], face_rcp(c[2]), face_rcp(c[5]), face_rcp(c[8]));
                 rec[3] = make_float4(face_rcp(c[2] + 1e-10f), face_rcp(c[5] + 1e-10f), face_rcp(c[8] + 1e-10f),
                                      __int_as_float(flags));
+#endif
                 if (fnorm) {
                     // face normal cross(v1 - v0, v2 - v1) (rasterize.py:166-170; torch.cross component order)
                     const float a0 = c[3] - c[0], a1 = c[4] - c[1], a2 = c[5] - c[2];

@@ -53,3 +53,25 @@ def test_bench_cli_two_ranks_gloo():
     assert res["allreduce_ms"] is not None and res["allreduce_ms"] > 0
     assert res["allreduce_bytes"] == 3 * 288 * 288 * 4
     assert res["value"] > 0 and res["steps"] == 3
+
+
+@pytest.mark.gpu
+def test_face_test_count_child():
+    """The forward's face-test counters (the -DNR_COUNT_TESTS build, bench.py's face-test rate, SURVEY
+    8d's secondary bound) through bench.py's own child: a forward of 8 ico-sphere items (level 3,
+    1280 faces) at 256^2 internal counts a positive number of (pixel, face) pass tests, 64 per face a
+    wave walks over an 8x8 block (no bin here is deep enough for 4x4 quarters), far below the brute
+    force's B S^2 F."""
+    sys.path.insert(0, ROOT)
+    import bench
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--count-child", "--batch", "8", "--level", "3",
+           "--image-size", "128"]
+    counts, note = bench.face_test_counts(cmd, timeout_s=150)
+    assert counts is not None, note
+    B, S, F = 8, 256, 1280
+    assert counts["tests"] > 0 and counts["tests"] == 64 * counts["walked"]
+    assert counts["walks"] > 0 and counts["commits"] > 0
+    assert counts["tests"] < B * S * S * F // 100
+    r = bench.face_test_rate(counts, note, B, S, F, 0.01)
+    assert r["tests_per_px"] == round(counts["tests"] / (B * S * S), 3)
+    assert r["brute_force_tests"] == B * S * S * F

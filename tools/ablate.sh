@@ -30,12 +30,12 @@ for V in $VARIANTS; do
   EV=""
   for d in ${V//,/ }; do case $d in @*) EV="$EV ${d#@}";; esac; done
   if [ -z "$NOHEAD" ]; then
-  env $EV NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --no-pmc > $OUT/bench_${i}_$r.log 2>&1
+  env $EV NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --no-pmc --no-count > $OUT/bench_${i}_$r.log 2>&1
   rc=$?; echo "$V rc=$rc: $(python -c "import json,sys; d=json.loads(open('$OUT/bench_${i}_$r.log').read().strip().splitlines()[-1]); print(d['kernels_ms'], d['ms_per_step'])")"
   if [ $rc -ne 0 ]; then exit $rc; fi
   fi
   if [ -n "$CONFIGS" ]; then
-    env $EV NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python tools/bench_configs.py --loop-steps 20 --only $CONFIGS > $OUT/configs_$i.log 2>&1
+    env $EV NR_LIB_PATH=$OUT/lib/libnr_$i.so timeout -k 10 300 python tools/bench_configs.py --loop-steps 20 --no-count --only $CONFIGS > $OUT/configs_$i.log 2>&1
     rc=$?; python -c "
 import json
 for l in open('$OUT/configs_$i.log'):

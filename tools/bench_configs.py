@@ -68,8 +68,9 @@ def pipelined_step(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
-def kernels_ms(fn, n=5):
-    """Per-kernel HIP-event durations recorded by the library (nr_profile_*), averaged over n steps."""
+def kernels_ms(fn, n=5, run=4):
+    """Per-kernel HIP-event durations recorded by the library (nr_profile_*), averaged over n samples,
+    each the last of `run` back-to-back steps (bench.time_kernels: no idle GPU before a timed step)."""
     import ctypes
     from neural_renderer_v2_pytorch_amd import _lib
     names = ["k_tex_pack", "k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
@@ -78,7 +79,8 @@ def kernels_ms(fn, n=5):
     acc = {k: [] for k in names}
     try:
         for _ in range(n):
-            fn()
+            for _ in range(run):
+                fn()
             torch.cuda.synchronize()
             for k in names:
                 ms = ctypes.c_float()
@@ -365,7 +367,9 @@ def main():
     dev = torch.device("cuda", 0)
     for name in a.only.split(","):
         r = globals()[name](dev, a)
-        if not a.no_count and "k_raster_fwd" in r.get("kernels_ms", {}):
+        # (not under rocprofv3: the counter-build child would inherit the profiler's preload)
+        if not a.no_count and "k_raster_fwd" in r.get("kernels_ms", {}) and \
+                not any(k.startswith("ROCPROF") for k in os.environ):
             meta = dict(batch=r["batch"], image_size=r["image_size"], F=r["faces"])
             ftr = face_tests(name, r, meta)
             r["fwd_face_tests_per_px"] = ftr.get("tests_per_px")

@@ -18,7 +18,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 $OUT/bench.log | cut -c1-600
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-pmc > $OUT/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-pmc --no-count > $OUT/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 head -8 $OUT/kernel_stats.csv 2>/dev/null | cut -c1-200

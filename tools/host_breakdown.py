@@ -52,8 +52,20 @@ def teapot():
     return proj, tex, vt_d, ft_d, faces, g, B, s
 
 
+def headline():
+    """bench.py's headline workload (64 items, 5120 faces, 256^2): (proj, tex, vt, ft, faces, g, B, s)."""
+    import bench
+    sys.argv = [sys.argv[0]]
+    w = bench.workload(bench.parse(), 0, dev)
+    vt = w["params"]().vertices_textures[0]
+    ft = w["params"]().faces_textures
+    return w["proj"], w["tex"], vt, ft, w["faces"], w["g"], w["g"].shape[0], w["g"].shape[2]
+
+
 def main():
-    proj, tex, vt_d, ft_d, faces, g, B, s = teapot()
+    which = os.environ.get("HOST_WORKLOAD", "teapot")
+    proj, tex, vt_d, ft_d, faces, g, B, s = headline() if which == "headline" else teapot()
+    print("workload", which)
     out = {}
 
     def params():

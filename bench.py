@@ -243,31 +243,35 @@ def kernel_bytes(w, args, measured=None):
 KERNELS = ["k_tex_pack", "k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
 
 
-def time_kernels(w, n=10, run=4):
+def time_kernels(w, n=20):
     """Per-kernel durations from HIP events the library records on its launch stream around each
-    launch (nr_profile_enable/read; each launch's pair overwrites the previous one's), averaged over n
-    samples.  Each sample is the last of `run` back-to-back steps, so the kernels it times run as in
-    the timed loop, behind other steps' work: a synchronisation before every sampled step leaves the
-    GPU idle for the host's enqueue time, and after such gaps the same kernels measured ~7 % slower
-    (round 6: bwd 0.208 against 0.193 ms by the rocprofv3 trace of a pipelined run on one box; the
-    memory side's power state, tools/warm_probe.py)."""
+    launch (nr_profile_enable/read: a ring of event pairs per kernel, averaged), over n steps run back
+    to back as in the timed loop, after 4 warm-up steps with the events on.  (Round 6: sampled one
+    step at a time, with a synchronisation before each, the same kernels measured 5-7 % slower than in
+    a rocprofv3 trace of a pipelined run on two boxes: the GPU idles for the host's enqueue time before
+    every sampled step, and its memory side leaves its busy state, tools/warm_probe.py.)"""
     import ctypes
     from neural_renderer_v2_pytorch_amd import _lib
     L = _lib.lib()
     _lib.check(L.nr_profile_enable(1), "nr_profile_enable")
-    acc = {k: [] for k in KERNELS}
+    res = {}
     try:
+        for _ in range(4):
+            step(w)
+        torch.cuda.synchronize()
+        _lib.check(L.nr_profile_enable(1), "nr_profile_enable")  # a new measurement: the n steps only
+        t0 = time.perf_counter()
         for _ in range(n):
-            for _ in range(run):
-                step(w)
-            torch.cuda.synchronize()
-            for k in KERNELS:
-                ms = ctypes.c_float()
-                if L.nr_profile_read(k.encode(), ctypes.byref(ms)) == 0:
-                    acc[k].append(ms.value)
+            step(w)
+        torch.cuda.synchronize()
+        res["_loop_ms_per_step"] = (time.perf_counter() - t0) / n * 1e3
+        for k in KERNELS:
+            ms = ctypes.c_float()
+            if L.nr_profile_read(k.encode(), ctypes.byref(ms)) == 0:
+                res[k] = float(ms.value)
     finally:
         L.nr_profile_enable(0)
-    return {k: float(np.mean(v)) for k, v in acc.items() if v}
+    return res
 
 
 def copy_ceiling_gbs(dev, nbytes=1 << 30, reps=10):
@@ -565,12 +569,10 @@ def main():
         host_single = (time.perf_counter() - t1) / args.steps * 1e3
         torch.cuda.synchronize()
 
-    # the host's own cost of enqueueing one step: with the GPU idle before each step (synchronised), so
-    # that no launch waits for queue space.  host_ms_per_step above is measured inside the timed loop,
-    # where the host runs ahead of the GPU until the runtime's launch queue is full and then waits for
-    # it: it includes that back-pressure and so rises toward the GPU step time on any box (0.21-0.31 ms
-    # on two boxes whose idle-GPU enqueue of the same step took ~0.1 ms, round 6), which is why it is
-    # not the host's cost.
+    # the host's own cost of enqueueing one step, with the GPU idle before each step (synchronised), so
+    # that no launch could wait for queue space: a check on host_ms_per_step above, which is measured
+    # inside the timed loop (the two agree on the boxes measured in round 6: the loop is not throttled
+    # by the launch queue)
     host_idle = []
     for _ in range(10):
         torch.cuda.synchronize()
@@ -607,6 +609,7 @@ def main():
 
     del images
     kms = time_kernels(w)
+    timing_loop_ms = kms.pop("_loop_ms_per_step", None)
     kb, total_bytes = kernel_bytes(w, args, kms)
     dominant = max(kms, key=kms.get)
     dom_ms, dom_bytes = kms[dominant], kb[dominant]
@@ -689,6 +692,8 @@ def main():
                 "valu_busy": round(pmc.get("valu_busy", {}).get(k, 0.0), 4),
                 "wait_share": round(pmc.get("wait_any_share", {}).get(k, 0.0), 4)} for k in pmc["hbm_bytes_per_launch"]},
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
+        # the step time of the loop kernels_ms was measured over (its HIP events on), beside ms_per_step
+        "kernels_ms_loop_ms_per_step": None if timing_loop_ms is None else round(timing_loop_ms, 4),
         # the forward's compute side in the contract's own unit: face tests per internal pixel and per
         # second (counter build), beside the brute force's B S^2 F
         "fwd_face_tests_per_px": None if ftr is None else ftr.get("tests_per_px"),

@@ -271,9 +271,11 @@ NR_API int nr_selftest_division(const float* a, const float* b, float* q_fast, f
 
 /* Measurement hook (bench.py's roofline leg; no reference counterpart).  With profiling on, the
  * library brackets each launch of its kernels with a pair of HIP events recorded on the launch
- * stream; nr_profile_read gives the duration in ms of the most recent launch of `kernel`
- * ("k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out", "k_tex_pack") once
- * the stream has been synchronised.  Process-wide state, meant for a single measuring thread. */
+ * stream; nr_profile_read gives the mean duration in ms of the launches of `kernel` ("k_face_setup",
+ * "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out", "k_tex_pack") recorded
+ * since profiling was last enabled (up to the last 64), once the stream has been synchronised;
+ * nr_profile_enable(1) while on starts a new measurement.  Process-wide state, meant for a single
+ * measuring thread. */
 NR_API int nr_profile_enable(int on);
 NR_API int nr_profile_read(const char* kernel, float* ms);
 

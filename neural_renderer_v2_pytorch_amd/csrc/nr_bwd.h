@@ -300,6 +300,8 @@ __global__ __launch_bounds__(2 * NT / NPX) __attribute__((amdgpu_waves_per_eu((F
 
     // halo ring from the forward's halo cache: asynchronous global -> LDS loads by waves 0 and 1
     // (lane t < NHALO carries halo pixel t, ring order of halo_pixel), landed before the barrier
+    // (round 6: dealt to all four waves, 25 each, so that no wave waits at the barrier for two others'
+    // moves: backward 0.2021-0.2033 against 0.1995-0.2029 ms, gpurun_out/hs; not kept)
     float(*s_hI)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4);
     float(*s_hG)[128] = reinterpret_cast<float(*)[128]>(s_raw + BWD_LDS_IG / 4 + MAXC * 128);
     // the halo pixel's bin flag: the forward writes no halo values for a bin without candidate faces
@@ -948,16 +950,16 @@ void launch_bwd_v(dim3 grid, hipStream_t st, const BwdArgs& ba, const Geom& g, c
     const bool one = (long long)grid.x * grid.y < 8192;
     const int hotf = HOT ? NR_LAUNCH_HOT_WINDOWS : 0;
     if (one) {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 1, 0, HOT>), grid, dim3(2 * NT), 0, st, ba, g, sh);
+        nr_launch((k_raster_bwd<FEAT, 1, 0, HOT>), grid, dim3(2 * NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{2 * NT, hotf});
     } else if (FEAT == 0 && sh.C == MAXC && ba.aa && ba.step_pow2) {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, MAXC, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
+        nr_launch((k_raster_bwd<FEAT, 2, MAXC, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     } else if (FEAT == 0 && sh.draw == static_draw(4) && ba.aa && ba.step_pow2) {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, 4, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
+        nr_launch((k_raster_bwd<FEAT, 2, 4, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_STATIC_CHANNELS | NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     } else {
-        hipLaunchKernelGGL((k_raster_bwd<FEAT, 2, 0, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
+        nr_launch((k_raster_bwd<FEAT, 2, 0, HOT>), grid, dim3(NT), 0, st, ba, g, sh);
         g_last_bwd.store(LaunchRec{NT, NR_LAUNCH_TWO_PX_PER_LANE | hotf});
     }
 }

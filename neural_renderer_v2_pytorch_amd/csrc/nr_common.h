@@ -55,8 +55,11 @@ enum { P_SETUP, P_RASTER, P_SHADE, P_BWD, P_VGRAD, P_TEXOUT, P_TEXPACK, P_N };
 const char* const kProfNames[P_N] = {"k_face_setup", "k_raster_fwd", "k_shade",
                                      "k_raster_bwd", "k_vertex_grad", "k_tex_out", "k_tex_pack"};
 bool g_prof = false;
-hipEvent_t g_prof_ev[P_N][2];
-bool g_prof_rec[P_N];
+// a ring of start/end event pairs per kernel: nr_profile_read averages the launches recorded since
+// profiling was (re)enabled, up to the last PROF_RING of them
+constexpr int PROF_RING = 64;
+hipEvent_t g_prof_ev[P_N][PROF_RING][2];
+int g_prof_n[P_N];
 
 // launch record (nr_last_launch): block size and NR_LAUNCH_* flags of the latest raster launches in
 // this process (process-wide: torch runs a backward on its autograd device thread), so tests can
@@ -78,16 +81,46 @@ struct LaunchSlot {
 };
 LaunchSlot g_last_fwd, g_last_bwd;
 
-struct ProfScope {  // records the start/end events of one launch when profiling is on
-    int k;
+// A launch's start / stop events for the next nr_launch of this thread (armed by a ProfScope of a single
+// launch): hipExtLaunchKernel stamps them from the kernel's own dispatch, where a pair of hipEventRecord
+// markers around the launch measured the headline's kernels 5-7 % longer than a rocprofv3 trace of the
+// same run on some boxes (round 6)
+thread_local hipEvent_t t_launch_ev[2] = {nullptr, nullptr};
+template <typename F, typename... Args>
+void nr_launch(F kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, Args... args) {
+    if (t_launch_ev[0]) {
+        hipEvent_t a = t_launch_ev[0], b = t_launch_ev[1];
+        t_launch_ev[0] = t_launch_ev[1] = nullptr;
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, st, a, b, 0u, args...);
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+    }
+}
+// Profiles the launches in its scope when profiling is on.  single: the scope holds one kernel
+// launch (nr_launch), which records its own start / stop; otherwise a pair of event markers brackets
+// the scope (the split forward's two streams, the backward with its window reduction)
+struct ProfScope {
+    int k, slot;
     hipStream_t st;
-    ProfScope(int k_, hipStream_t s) : k(k_), st(s) {
-        if (g_prof) (void)hipEventRecord(g_prof_ev[k][0], st);
+    bool single;
+    ProfScope(int k_, hipStream_t s, bool single_ = false) : k(k_), slot(g_prof_n[k_] % PROF_RING), st(s), single(single_) {
+        if (!g_prof) return;
+        if (single) {
+            t_launch_ev[0] = g_prof_ev[k][slot][0];
+            t_launch_ev[1] = g_prof_ev[k][slot][1];
+        } else {
+            (void)hipEventRecord(g_prof_ev[k][slot][0], st);
+        }
     }
     ~ProfScope() {
-        if (g_prof) {
-            (void)hipEventRecord(g_prof_ev[k][1], st);
-            g_prof_rec[k] = true;
+        if (!g_prof) return;
+        if (single) {
+            const bool launched = t_launch_ev[0] == nullptr;
+            t_launch_ev[0] = t_launch_ev[1] = nullptr;
+            if (launched) g_prof_n[k]++;
+        } else {
+            (void)hipEventRecord(g_prof_ev[k][slot][1], st);
+            g_prof_n[k]++;
         }
     }
 };

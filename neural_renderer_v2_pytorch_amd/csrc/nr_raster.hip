@@ -26,6 +26,7 @@
 // halo cache, standalone reference kernels), nr_bwd.h (backward), nr_camera.h (look_at + perspective),
 // nr_host.h (argument checks); this file holds the extern "C" ABI.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <limits.h>
 #include <math.h>
@@ -188,8 +189,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     // setup launch, or a texture too large for that, the repacking gets a launch of its own
     const long long setup_idle = (long long)((F + SETUP_FACES - 1) / SETUP_FACES) * B * (256 - SETUP_FACES);
     if (pk.out && (F == 0 || pk.n > 32 * setup_idle)) {
-        ProfScope _p(P_TEXPACK, st);
-        hipLaunchKernelGGL(k_tex_pack, dim3((unsigned)((pk.n + 255) / 256)), dim3(256), 0, st, pk);
+        ProfScope _p(P_TEXPACK, st, true);
+        nr_launch(k_tex_pack, dim3((unsigned)((pk.n + 255) / 256)), dim3(256), 0, st, pk);
         const int e = check_launch("k_tex_pack");
         if (e) return e;
         pk.out = nullptr;
@@ -201,25 +202,25 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         dim3 grid((F + SETUP_FACES - 1) / SETUP_FACES, B);
         const bool rgb = ra && (ra->draw_flags & NR_DRAW_RGB);
         const int uv_items = rgb ? (ra->vt_batch_stride ? B : 1) : 0;
-        ProfScope _p(P_SETUP, st);
+        ProfScope _p(P_SETUP, st, true);
         const bool lit = rgb && ra->num_lights > 0;
         const size_t lds = (size_t)setup_lds_words(g.nbins) * 4;
         if (vertices)
-            hipLaunchKernelGGL(k_face_setup<true>, grid, dim3(256), lds, st, vertices, faces_idx, face_records, V, F, S,
+            nr_launch(k_face_setup<true>, grid, dim3(256), lds, st, vertices, faces_idx, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords,
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
                                rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk, zf,
                                ordered ? bin_part : nullptr, B % 8 == 0);
         else
-            hipLaunchKernelGGL(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
+            nr_launch(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
                                nullptr, pk, zf, ordered ? bin_part : nullptr, B % 8 == 0);
         int e = check_launch("k_face_setup");
         if (e) return e;
         if (lit && V > 0) {
             const long long nv = (long long)B * V;
-            hipLaunchKernelGGL(k_vertex_normals, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, ra->face_normals,
+            nr_launch(k_vertex_normals, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, ra->face_normals,
                                ra->normal_offsets, ra->normal_faces, ra->vertex_normals, F, V, nv);
             e = check_launch("k_vertex_normals");
             if (e) return e;
@@ -251,7 +252,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     // gpurun_out/e7, e9)
     const int deep_cap = min(Bcap / 8 * g.nbins, deep_slots_per_xcd() * 7 / 8);
     if (ordered) {
-        hipLaunchKernelGGL(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,
+        nr_launch(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,
                            g.nbins, side ? split_cnt : nullptr, SPLIT_BUCKET, deep_cap);
         const int e = check_launch("k_bin_order");
         if (e) return e;
@@ -263,7 +264,7 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     // shading nothing else in this launch reads them, and the backward skips those tiles by the flags
     const int sparse = (ra && ra->face_index_sparse && fuse && binfg) ? 1 : 0;
     {
-        ProfScope _p(P_RASTER, st);
+        ProfScope _p(P_RASTER, st, side == nullptr);
         const int rs = vertices ? FACE_REC : 9;
         g_last_fwd.store(LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
                                         (fuse && ntf == 256 && (sh.C == MAXC || sh.draw == static_draw(4)) ? NR_LAUNCH_STATIC_CHANNELS : 0) |
@@ -276,71 +277,71 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                 return check_launch("hipEventRecord");
             // (a grid of exactly the cap's blocks: every block past a list's deep prefix exits at once, but
             // each still needs a 1024-thread slot to be dispatched in)
-            hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(8 * deep_cap), dim3(1024), 0, st, face_records, rs, bbox,
+            nr_launch((k_raster_fwd<1024, true>), dim3(8 * deep_cap), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 1);
             int e = check_launch("k_raster_fwd");
             if (e) return e;
             if (sh.C == MAXC)
-                hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
+                nr_launch((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
                                    bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
                                    split_cnt, 2);
             else if (sh.draw == static_draw(4))  // rgba (the car): compile-time channels
-                hipLaunchKernelGGL((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
+                nr_launch((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
                                    bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
                                    split_cnt, 2);
             else
-                hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs, bbox,
+                nr_launch((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs, bbox,
                                    mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 2);
             e = check_launch("k_raster_fwd");
             if (e) return e;
             if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess)
                 return check_launch("hipEventRecord");
         } else if (fuse && ntf == 1024 && ordered)  // deep bins, not split (e.g. one item): dealt quarters
-            hipLaunchKernelGGL((k_raster_fwd<1024, true, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
+            nr_launch((k_raster_fwd<1024, true, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
                                bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse && ntf == 1024)
-            hipLaunchKernelGGL((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
+            nr_launch((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
-            hipLaunchKernelGGL((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
+            nr_launch((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse && sh.draw == static_draw(4))  // rgba: compile-time channels
-            hipLaunchKernelGGL((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
+            nr_launch((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (fuse)
-            hipLaunchKernelGGL((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
+            nr_launch((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
                                F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
         else if (ntf == 256)
-            hipLaunchKernelGGL((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
+            nr_launch((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
                                F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
         else if (ordered)
-            hipLaunchKernelGGL((k_raster_fwd<1024, false, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
+            nr_launch((k_raster_fwd<1024, false, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
                                bbox, mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
         else
-            hipLaunchKernelGGL((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
+            nr_launch((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra || fuse) return e;
     const int s = ra->anti_aliasing ? S / 2 : S;
     {
-        ProfScope _p(P_SHADE, st);
+        ProfScope _p(P_SHADE, st, true);
         if (((long long)s * s + 255) / 256 * B < 4096) {
             const dim3 grid((unsigned)(((long long)s * s + (ra->anti_aliasing ? 63 : 255)) / (ra->anti_aliasing ? 64 : 256)), B);
             switch ((sh.nl ? 1 : 0) | (sh.bg ? 2 : 0)) {
-                case 0: hipLaunchKernelGGL(k_shade_px<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
-                case 1: hipLaunchKernelGGL(k_shade_px<1>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
-                case 2: hipLaunchKernelGGL(k_shade_px<2>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
-                default: hipLaunchKernelGGL(k_shade_px<3>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+                case 0: nr_launch(k_shade_px<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+                case 1: nr_launch(k_shade_px<1>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+                case 2: nr_launch(k_shade_px<2>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+                default: nr_launch(k_shade_px<3>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
             }
             return check_launch("k_shade");
         }
         const dim3 grid((unsigned)(((long long)s * s + 255) / 256), B);
         switch ((sh.nl ? 1 : 0) | (sh.bg ? 2 : 0)) {
-            case 0: hipLaunchKernelGGL(k_shade<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
-            case 1: hipLaunchKernelGGL(k_shade<1>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
-            case 2: hipLaunchKernelGGL(k_shade<2>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
-            default: hipLaunchKernelGGL(k_shade<3>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            case 0: nr_launch(k_shade<0>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            case 1: nr_launch(k_shade<1>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            case 2: nr_launch(k_shade<2>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
+            default: nr_launch(k_shade<3>, grid, dim3(256), 0, st, face_records, fim, F, S, sh, ra->anti_aliasing, images, ra->halo); break;
         }
     }
     return check_launch("k_shade");
@@ -367,7 +368,7 @@ int nr_compute_weight_map(const float* faces, const int32_t* face_index_map, flo
         return fail(NR_ERR_ARGS, "bad sizes B=%d F=%d S=%d", batch_size, num_faces, image_size);
     const long long n = (long long)batch_size * image_size * image_size;
     if (n == 0) return NR_OK;
-    hipLaunchKernelGGL(k_weight_map, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, faces,
+    nr_launch(k_weight_map, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, faces,
                        face_index_map, weight_map, num_faces, image_size, n);
     return check_launch("k_weight_map");
 }
@@ -376,7 +377,7 @@ int nr_mask_foreground_forward(const int32_t* face_index, const float* data_in, 
                                void* stream) {
     if (n < 0 || dim < 0) return fail(NR_ERR_ARGS, "bad sizes");
     if (n == 0) return NR_OK;
-    hipLaunchKernelGGL(k_mask_fg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, face_index,
+    nr_launch(k_mask_fg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, face_index,
                        data_in, data_out, n, dim);
     return check_launch("k_mask_fg");
 }
@@ -392,7 +393,7 @@ int nr_differentiation_backward(const float* images, const float* grad, float* g
     const long long n = (long long)batch_size * height * width;
     if (n == 0) return NR_OK;
     const float step = (float)(2. / height);
-    hipLaunchKernelGGL(k_diff_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, images, grad,
+    nr_launch(k_diff_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, images, grad,
                        grad_xy, height, width, channels, step, n);
     return check_launch("k_diff_bwd");
 }
@@ -547,7 +548,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     ba.hot_acc = hot ? a->hot_acc : nullptr;
     Shade sh = make_shade(a);
     {
-        ProfScope _p(P_BWD, st);
+        ProfScope _p(P_BWD, st, !hot);
         const dim3 grid(((S + TW - 1) / TW) * ((S + BH - 1) / BH), a->batch_size);
         const bool silo = !(a->draw_flags & (NR_DRAW_RGB | NR_DRAW_DEPTH));  // lights / backgrounds need rgb
         switch ((lit ? 1 : 0) | (sh.bg ? 2 : 0) | (silo ? 4 : 0)) {
@@ -563,7 +564,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
         // complete; bench.py counts their bytes there), before the texture-gradient output (k_vertex_grad
         // / k_tex_out) reads the accumulator
         if (hot) {
-            hipLaunchKernelGGL(k_hot_reduce, dim3((unsigned)a->num_hot), dim3(64), 0, st, a->hot_acc, a->num_hot, g4,
+            nr_launch(k_hot_reduce, dim3((unsigned)a->num_hot), dim3(64), 0, st, a->hot_acc, a->num_hot, g4,
                                a->tex_width, a->tex_height);
             e = check_launch("k_hot_reduce");
             if (e) return e;
@@ -572,13 +573,13 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     const long long nv = (long long)a->batch_size * a->num_vertices;
     if (lit && nv > 0) {
         // lights: vertex-normal gradients -> face normals -> corner gradients (added into gF)
-        hipLaunchKernelGGL(k_vnormal_bwd, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gN, a->vertex_offsets,
+        nr_launch(k_vnormal_bwd, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, gN, a->vertex_offsets,
                            a->vertex_faces, a->vertex_normals, gU, a->num_faces, a->num_vertices, nv);
         e = check_launch("k_vnormal_bwd");
         if (e) return e;
         const long long nf = (long long)a->batch_size * a->num_faces;
         if (nf > 0) {
-            hipLaunchKernelGGL(k_fnormal_bwd, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, a->face_records,
+            nr_launch(k_fnormal_bwd, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, a->face_records,
                                a->faces, gU, gF, a->num_faces, a->num_vertices, nf);
             e = check_launch("k_fnormal_bwd");
             if (e) return e;
@@ -597,7 +598,7 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     // 0.022 + 0.0135 -> 0.031 ms; at 8 it had a launch of its own; same-box A/B, gpurun_out/o28)
     const bool carry = nv > 0 && to.n <= 16 * vgrad_threads;
 #ifdef NR_ABL_EXTRAK
-    hipLaunchKernelGGL(k_abl_empty, dim3(NR_ABL_EXTRAK), dim3(256), 0, st, 0);
+    nr_launch(k_abl_empty, dim3(NR_ABL_EXTRAK), dim3(256), 0, st, 0);
 #endif
 #ifdef NR_ABL_NOVGRAD
     if (false) {
@@ -605,8 +606,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     if (nv > 0) {
 #endif
         {
-            ProfScope _p(P_VGRAD, st);
-            hipLaunchKernelGGL(k_vertex_grad, dim3((unsigned)vblocks), dim3(VB), 0, st, gF, a->vertex_offsets,
+            ProfScope _p(P_VGRAD, st, true);
+            nr_launch(k_vertex_grad, dim3((unsigned)vblocks), dim3(VB), 0, st, gF, a->vertex_offsets,
                                a->vertex_faces, grad_vertices, a->num_faces, a->num_vertices, nv, carry ? to : TexOut{},
                                xcd_items);
         }
@@ -615,8 +616,8 @@ int nr_rasterize_backward(const NrRasterArgs* a, const float* grad_images, float
     }
     if (to.out && to.n > 0 && !carry) {
         {
-            ProfScope _p(P_TEXOUT, st);
-            hipLaunchKernelGGL(k_tex_out, dim3((unsigned)((to.n + 255) / 256)), dim3(256), 0, st, to);
+            ProfScope _p(P_TEXOUT, st, true);
+            nr_launch(k_tex_out, dim3((unsigned)((to.n + 255) / 256)), dim3(256), 0, st, to);
         }
         e = check_launch("k_tex_out");
     }
@@ -657,13 +658,13 @@ int nr_rasterize_backward_params(const NrRasterArgs* a, const float* grad_images
     const Shade sh = make_shade(a);  // the lights shade (cw) the uv gradient even without light gradients
     const dim3 grid((unsigned)(((long long)S * S + 255) / 256), B);
     if (uv && lgt)
-        hipLaunchKernelGGL((k_param_bwd<true, true>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
+        nr_launch((k_param_bwd<true, true>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
                            grad_vertices_textures, gvt_bstride, grad_lights);
     else if (uv)
-        hipLaunchKernelGGL((k_param_bwd<true, false>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
+        nr_launch((k_param_bwd<true, false>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
                            grad_vertices_textures, gvt_bstride, grad_lights);
     else
-        hipLaunchKernelGGL((k_param_bwd<false, true>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
+        nr_launch((k_param_bwd<false, true>), grid, dim3(256), 0, st, ba, sh, S, a->faces_textures,
                            grad_vertices_textures, gvt_bstride, grad_lights);
     return check_launch("k_param_bwd");
 }
@@ -685,7 +686,7 @@ int nr_camera_forward(const NrCameraArgs* c, float* out, void* stream) {
     const long long n = (long long)c->batch_size * c->num_vertices;
     if (n == 0) return NR_OK;
     if (!out) return fail(NR_ERR_ARGS, "null output");
-    hipLaunchKernelGGL(k_camera_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *c, out);
+    nr_launch(k_camera_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *c, out);
     return check_launch("k_camera_fwd");
 }
 
@@ -716,13 +717,13 @@ int nr_camera_backward(const NrCameraArgs* c, const float* grad_out, float* grad
         if (hipMemsetAsync(acc, 0, (size_t)c->batch_size * 12 * 4, st) != hipSuccess) return check_launch("hipMemsetAsync");
     }
     if ((grad_vertices || acc) && nv > 0) {
-        hipLaunchKernelGGL(k_camera_bwd, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, *c, grad_out, grad_vertices, acc);
+        nr_launch(k_camera_bwd, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, *c, grad_out, grad_vertices, acc);
         e = check_launch("k_camera_bwd");
         if (e) return e;
     }
     if (want_eye) {
         if (nv == 0 && hipMemsetAsync(acc, 0, (size_t)c->batch_size * 12 * 4, st) != hipSuccess) return check_launch("hipMemsetAsync");
-        hipLaunchKernelGGL(k_camera_eye, dim3((unsigned)((neye + 63) / 64)), dim3(64), 0, st, *c, acc, grad_eye);
+        nr_launch(k_camera_eye, dim3((unsigned)((neye + 63) / 64)), dim3(64), 0, st, *c, acc, grad_eye);
         e = check_launch("k_camera_eye");
     }
     return e;
@@ -731,7 +732,7 @@ int nr_camera_backward(const NrCameraArgs* c, const float* grad_out, float* grad
 int nr_selftest_division(const float* a, const float* b, float* q_fast, float* q_ieee, long long n, void* stream) {
     if (n < 0 || (n > 0 && (!a || !b || !q_fast || !q_ieee))) return fail(NR_ERR_ARGS, "bad arguments");
     if (n == 0) return NR_OK;
-    hipLaunchKernelGGL(k_selftest_div, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a, b,
+    nr_launch(k_selftest_div, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a, b,
                        q_fast, q_ieee, n);
     return check_launch("k_selftest_div");
 }
@@ -777,14 +778,16 @@ int nr_last_launch(const char* kernel, int* block_threads, int* flags) {
 int nr_profile_enable(int on) {
     if (on && !g_prof) {
         for (int k = 0; k < P_N; k++)
-            for (int j = 0; j < 2; j++)
-                if (hipEventCreate(&g_prof_ev[k][j]) != hipSuccess) return fail(NR_ERR_LAUNCH, "hipEventCreate failed");
+            for (int r = 0; r < PROF_RING; r++)
+                for (int j = 0; j < 2; j++)
+                    if (hipEventCreate(&g_prof_ev[k][r][j]) != hipSuccess) return fail(NR_ERR_LAUNCH, "hipEventCreate failed");
     } else if (!on && g_prof) {
         for (int k = 0; k < P_N; k++)
-            for (int j = 0; j < 2; j++) (void)hipEventDestroy(g_prof_ev[k][j]);
+            for (int r = 0; r < PROF_RING; r++)
+                for (int j = 0; j < 2; j++) (void)hipEventDestroy(g_prof_ev[k][r][j]);
     }
-    if (!on || !g_prof)
-        for (int k = 0; k < P_N; k++) g_prof_rec[k] = false;
+    // (re)enabling starts a new measurement: the ring's recorded launches are forgotten
+    for (int k = 0; k < P_N; k++) g_prof_n[k] = 0;
     g_prof = on != 0;
     return NR_OK;
 }
@@ -807,9 +810,16 @@ int nr_profile_read(const char* kernel, float* ms) {
     if (!kernel || !ms) return fail(NR_ERR_ARGS, "null argument");
     for (int k = 0; k < P_N; k++) {
         if (strcmp(kernel, kProfNames[k]) != 0) continue;
-        if (!g_prof || !g_prof_rec[k]) return fail(NR_ERR_ARGS, "%s: no profiled launch recorded", kernel);
-        if (hipEventElapsedTime(ms, g_prof_ev[k][0], g_prof_ev[k][1]) != hipSuccess)
-            return fail(NR_ERR_LAUNCH, "%s: hipEventElapsedTime failed", kernel);
+        if (!g_prof || g_prof_n[k] == 0) return fail(NR_ERR_ARGS, "%s: no profiled launch recorded", kernel);
+        const int n = g_prof_n[k] < PROF_RING ? g_prof_n[k] : PROF_RING;
+        double sum = 0.0;
+        for (int r = 0; r < n; r++) {
+            float e = 0.f;
+            if (hipEventElapsedTime(&e, g_prof_ev[k][r][0], g_prof_ev[k][r][1]) != hipSuccess)
+                return fail(NR_ERR_LAUNCH, "%s: hipEventElapsedTime failed", kernel);
+            sum += e;
+        }
+        *ms = (float)(sum / n);
         return NR_OK;
     }
     return fail(NR_ERR_ARGS, "unknown kernel name %s", kernel);

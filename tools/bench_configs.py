@@ -68,27 +68,30 @@ def pipelined_step(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
-def kernels_ms(fn, n=5, run=4):
-    """Per-kernel HIP-event durations recorded by the library (nr_profile_*), averaged over n samples,
-    each the last of `run` back-to-back steps (bench.time_kernels: no idle GPU before a timed step)."""
+def kernels_ms(fn, n=10):
+    """Per-kernel HIP-event durations recorded by the library (nr_profile_*, its ring of event pairs
+    averaged) over n steps run back to back after 3 warm-up steps (bench.time_kernels)."""
     import ctypes
     from neural_renderer_v2_pytorch_amd import _lib
     names = ["k_tex_pack", "k_face_setup", "k_raster_fwd", "k_shade", "k_raster_bwd", "k_vertex_grad", "k_tex_out"]
     L = _lib.lib()
     _lib.check(L.nr_profile_enable(1), "nr_profile_enable")
-    acc = {k: [] for k in names}
+    res = {}
     try:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        _lib.check(L.nr_profile_enable(1), "nr_profile_enable")
         for _ in range(n):
-            for _ in range(run):
-                fn()
-            torch.cuda.synchronize()
-            for k in names:
-                ms = ctypes.c_float()
-                if L.nr_profile_read(k.encode(), ctypes.byref(ms)) == 0:
-                    acc[k].append(ms.value)
+            fn()
+        torch.cuda.synchronize()
+        for k in names:
+            ms = ctypes.c_float()
+            if L.nr_profile_read(k.encode(), ctypes.byref(ms)) == 0:
+                res[k] = round(float(ms.value), 5)
     finally:
         L.nr_profile_enable(0)
-    return {k: round(float(np.mean(v)), 5) for k, v in acc.items() if v}
+    return res
 
 
 def graphed(step):

@@ -288,7 +288,8 @@ enum { NR_LAUNCH_FUSED_SHADE = 1, NR_LAUNCH_STATIC_CHANNELS = 2, NR_LAUNCH_TWO_P
        NR_LAUNCH_DEEP_FIRST = 8 /* k_raster_fwd: bins dispatched deepest first (k_bin_order) */,
        NR_LAUNCH_SPLIT = 16 /* k_raster_fwd: deep bins at 1024 threads, the rest at 256 on a side stream */,
        NR_LAUNCH_HOT_WINDOWS = 32 /* k_raster_bwd: shared texture windows into private copies (face_hot) */,
-       NR_LAUNCH_DEALT_QUARTERS = 64 /* k_raster_fwd: deep bins' 4x4 quarters dealt to the waves (not split) */ };
+       NR_LAUNCH_DEALT_QUARTERS = 64 /* k_raster_fwd: deep bins' 4x4 quarters dealt to the waves (not split) */,
+       NR_LAUNCH_QUADRANTS = 128 /* k_raster_fwd: deep bins walked by four blocks, one per 16x16 quadrant (not split) */ };
 NR_API int nr_last_launch(const char* kernel, int* block_threads, int* flags);
 
 #ifdef NR_COUNT_TESTS

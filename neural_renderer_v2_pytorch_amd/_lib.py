@@ -31,7 +31,7 @@ EXPORTS = [
 ABI_VERSION = 6  # include/nr_raster.h NR_ABI_VERSION
 
 NR_LAUNCH_FUSED_SHADE, NR_LAUNCH_STATIC_CHANNELS, NR_LAUNCH_TWO_PX_PER_LANE, NR_LAUNCH_DEEP_FIRST, NR_LAUNCH_SPLIT = 1, 2, 4, 8, 16
-NR_LAUNCH_HOT_WINDOWS, NR_LAUNCH_DEALT_QUARTERS = 32, 64
+NR_LAUNCH_HOT_WINDOWS, NR_LAUNCH_DEALT_QUARTERS, NR_LAUNCH_QUADRANTS = 32, 64, 128
 NR_HOT_MAX, NR_HOT_COPIES = 256, 32
 
 c_int, c_float, c_void_p, c_size_t, c_ll = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_longlong

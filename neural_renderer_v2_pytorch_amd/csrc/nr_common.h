@@ -736,16 +736,32 @@ __device__ __forceinline__ void block_item_tile(int G, int nx, int ny, int& b, i
 // run_face_index).  Returns -1 past the block's part (the block ends), 1 when the entry carries
 // ORDER_EMPTY (no candidate face: the block skips the bin-mask scan), else 0.
 constexpr int ORDER_EMPTY = 1 << 30;
+// part 3 (quadrant split, a forward that does not split its list over two launches): the first
+// split[x] entries of list x (its bins of >= 512 candidates, deepest first) are each walked by four
+// blocks, one per 16x16 quadrant (quad 0-3: x half quad & 1, y half quad >> 1), the rest by one block
+// each (quad -1); the grid holds 3 cap blocks per list more than the list, the surplus exits
+// (QS: part 3 compiled in -- the dealt-quarter variant, the only one launched with it)
+template <bool QS>
 __device__ __forceinline__ int ordered_bin(const int* __restrict__ order, const int* __restrict__ split, int part, int B,
-                                           int nbins, int nbx, int& b, int& tx, int& ty) {
+                                           int nbins, int nbx, int& b, int& tx, int& ty, int& quad) {
     const int L = blockIdx.y * gridDim.x + blockIdx.x;
     const bool per_xcd = B % 8 == 0;
     const int x = per_xcd ? (L & 7) : 0;
     const int n = per_xcd ? (B >> 3) * nbins : B * nbins;
     int r = per_xcd ? (L >> 3) : L;
     int hi = n;
+    quad = -1;
     if (part == 1) hi = split[x];
     else if (part == 2) r += split[x];
+    else if (QS && part == 3) {
+        const int d = split[x];
+        if (r < 4 * d) {
+            quad = r & 3;
+            r >>= 2;
+        } else {
+            r -= 3 * d;
+        }
+    }
     if (r >= hi) return -1;
     const int oe = order[x * n + r];
     const int e = oe & (ORDER_EMPTY - 1);

@@ -564,6 +564,101 @@ __device__ __forceinline__ void walk_block(const float4* __restrict__ s_face, co
     if (pend >= 0) face_commit<FST, SLOT>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
 }
 
+// walk_block for one 4x4 quarter q (the dealt-quarter deep walk) with four faces per step: lane group
+// g = lane >> 4 runs the pass test of the step's g-th face (ballot order, so ascending) at pixel
+// lane & 15, every group holding the same 16 pixels (xp, yp, depth_min replicated by the caller).  The
+// groups' coverage masks then go through the pending-face logic one group at a time, in face order, on
+// the scalar unit: a face that passes at a pixel with a pending face commits the wave's pending faces
+// first, exactly as walk_block's sequential loop does, so every pixel still commits its faces in
+// ascending order (face_commit: lanes 0-15, whose depth_min and best are the pixels' own).  Groups 1-3
+// test against a copy of the depths taken before the step's commits -- a bound >= the pixel's current
+// minimum, as the pass test allows -- refreshed from lanes 0-15 after any commit.  With one face per
+// step lanes 16-63 sat idle through the quarter walk; this walks the deep bins' quarters in about a
+// quarter of the steps.
+template <int FST>
+__device__ __forceinline__ void walk_quarter4(const float4* __restrict__ s_face, const uint64_t* __restrict__ s_q, int q,
+                                              int n, int lane, float xp, float yp, float near, float far, float delta,
+                                              float& depth_min, int& best) {
+    int pend = -1;               // staging slot of my pixel's pending face (lanes 0-15)
+    unsigned long long occ = 0;  // the quarter's pixels (bits 0-15) with a pending face
+    float zmax = 0.f;
+    bool dirty = true;
+    const int g = lane >> 4;
+#ifdef NR_COUNT_TESTS
+    unsigned long long cnt_walked = 0, cnt_commits = 0;
+#endif
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        if (dirty && (c0 & NR_ZREFRESH) == 0) {  // (as walk_block's ZCULL)
+            zmax = wave_max(depth_min);
+            dirty = false;
+        }
+        bool hit = false;
+        if (c0 + lane < n) hit = ((s_q[c0 + lane] >> q) & 1) && !(s_face[FST + c0 + lane].x > zmax);
+        for (unsigned long long m = __ballot(hit); m;) {
+            int sl[4];
+            unsigned long long valid = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                sl[k] = m ? c0 + __builtin_ctzll(m) : c0;
+                valid |= m ? 0xffffull << (16 * k) : 0ull;
+                m &= m - 1;
+            }
+#ifdef NR_COUNT_TESTS
+            cnt_walked += __popcll(valid) >> 4;
+#endif
+            const int slot = g == 0 ? sl[0] : g == 1 ? sl[1] : g == 2 ? sl[2] : sl[3];
+            const float4* e = s_face + slot;
+            FaceRows<FST> fr;
+            fr.load(e);
+            const float4 q0 = fr.get(e, 0), q1 = fr.get(e, 1);
+            const unsigned long long pre = lane_mask_uge(depth_min, q1.x) & lane_mask_uge(xp, q0.x) &
+                                           lane_mask_ule(xp, q0.y) & lane_mask_uge(yp, q0.z) & lane_mask_ule(yp, q0.w) &
+                                           valid;
+            unsigned long long cov = 0;
+            if (pre) {
+                const float4 q2 = fr.get(e, 2), q3 = fr.get(e, 3), q4 = fr.get(e, 4);
+                const float c1 = (yp - q2.x) * q3.x - q3.z * (xp - q2.z);
+                const float c3 = (yp - q2.y) * q3.y - q3.w * (xp - q2.w);
+                const float c2 = (yp - q4.x) * q4.z - (xp - q4.y) * q4.w;
+                cov = lane_mask_uge(c1 * c2, 0.f) & lane_mask_uge(c3 * c2, 0.f) & pre;
+            }
+            if (cov) {
+                bool committed = false;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const unsigned long long ck = (cov >> (16 * k)) & 0xffffull;
+                    if (ck & occ) {
+#ifdef NR_COUNT_TESTS
+                        cnt_commits++;
+#endif
+                        if (pend >= 0) face_commit<FST, false>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
+                        pend = -1;
+                        occ = 0;
+                        committed = true;
+                    }
+                    int sv = sl[k];
+                    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(pend) : "v"(pend), "v"(sv), "s"(ck));
+                    occ |= ck;
+                }
+                if (committed) {
+                    depth_min = __shfl(depth_min, lane & 15);
+                    dirty = true;
+                }
+            }
+        }
+    }
+#ifdef NR_COUNT_TESTS
+    if (occ) cnt_commits++;
+    if (lane == 0) {
+        atomicAdd(&g_fwd_count[0], cnt_walked * 16ull);
+        atomicAdd(&g_fwd_count[1], cnt_walked);
+        atomicAdd(&g_fwd_count[2], cnt_commits);
+        atomicAdd(&g_fwd_count[3], 1ull);
+    }
+#endif
+    if (pend >= 0) face_commit<FST, false>(s_face, pend, xp, yp, near, far, delta, depth_min, best);
+}
+
 // Which of the bin's sixteen 8x8 pixel blocks a staged face may touch: bit 4 r + j (block column j, row
 // r of the 32x32 bin at (bx0, by0)) is set when the face's float bbox meets the block's pixel-centre
 // extent [pix_center(bx0 + 8 j), pix_center(bx0 + 8 j + 7)] x (the same in y) and, with CULL, its
@@ -740,8 +835,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
     const int S = g.S;
     int b, bin_x, bin_y;
     bool known_empty = false;  // (ordered) the setup's counts say the bin has no candidate face
+    int quad = -1;             // (part 3) this block walks one 16x16 quadrant of a deep bin
     if (order) {
-        const int ob = ordered_bin(order, split, part, g.B, g.nbins, g.nbx, b, bin_x, bin_y);
+        const int ob = ordered_bin<DQ>(order, split, part, g.B, g.nbins, g.nbx, b, bin_x, bin_y, quad);
         if (ob < 0) return;  // past this launch's part of the list (block-uniform, before any barrier)
         known_empty = ob == 1;
     } else {
@@ -840,7 +936,7 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                 if (px < S && py < S) fimb[(int)__umul24(py, S) + px] = id;
             }
         }
-    } else if (DQ && NTF >= 1024 && CULL && total0 >= ZCULL_MIN) {
+    } else if (DQ && NTF >= 1024 && CULL && (total0 >= ZCULL_MIN || quad >= 0)) {
         // dealt quarters (the deep bins of the 1024-thread variant): in each staging round the bin's 64
         // 4x4 quarters, longest face list first, are dealt to the 16 waves from a counter; a wave walks
         // one quarter at a time on lanes 0-15, its pixels' state (depth, winner) in LDS between rounds.
@@ -864,6 +960,14 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         s_dm[t] = far;
         s_best[t] = -1;
         quarter_extents(s_ext4, t, bx0, by0, S);
+        // a quadrant block (quad >= 0) keeps only its quadrant's 16 quarters in the staged masks
+        // (quarter q = 8 R + J: J < 4 in the left half, R < 4 in the top half), so the faces that miss
+        // the quadrant are never walked and the other quarters' lengths are 0 (never dealt); it stages
+        // every candidate as the whole-bin block does, and computes only its half of the mask rows
+        const uint64_t qkeep = quad < 0 ? ~0ull
+                                        : ((quad & 1) ? 0xF0F0F0F0F0F0F0F0ull : 0x0F0F0F0F0F0F0F0Full) &
+                                              ((quad & 2) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull);
+        const bool rows_lo = quad < 0 || !(quad & 2), rows_hi = quad < 0 || (quad & 2);
         uint32_t bits = bits0;
         int total = total0, off = off0;
         for (int wbase = 0;;) {
@@ -888,10 +992,13 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                     if (t < n) {
                         const float* c = frb + s_cand[j0 + t] * rs;
                         stage_face<FCAP, CULL, false>(s_face, nullptr, t, c, s_cand[j0 + t], nullptr, false);
-                        reinterpret_cast<uint32_t*>(s_q)[2 * t] = face_quarter_mask<CULL>(c, s_ext4, 0);
+                        reinterpret_cast<uint32_t*>(s_q)[2 * t] =
+                            rows_lo ? face_quarter_mask<CULL>(c, s_ext4, 0) & (uint32_t)qkeep : 0u;
                     } else if (t >= FCAP && t - FCAP < n) {
                         reinterpret_cast<uint32_t*>(s_q)[2 * (t - FCAP) + 1] =
-                            face_quarter_mask<CULL>(frb + s_cand[j0 + t - FCAP] * rs, s_ext4, 4);
+                            rows_hi ? face_quarter_mask<CULL>(frb + s_cand[j0 + t - FCAP] * rs, s_ext4, 4) &
+                                          (uint32_t)(qkeep >> 32)
+                                    : 0u;
                     }
                     if (t == 0) s_next = 0;
                     __syncthreads();
@@ -928,11 +1035,19 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                         const int px = (q & 7) * 4 + (lane & 3), py = (q >> 3) * 4 + ((lane >> 2) & 3);
                         const bool on = lane < 16;
                         const int pix = py * COARSE + px;
+#ifndef NR_NO_W4
+                        float dm = s_dm[pix];  // (lanes 16-63: copies of lanes 0-15, walk_quarter4)
+#else
                         float dm = on ? s_dm[pix] : -INFINITY;  // lanes 16-63: no pixel (and no share of the wave's depth maximum)
+#endif
                         int best = on ? s_best[pix] : -1;
                         const float xq = pix_center_div(bx0 + px, S), yq = pix_center_div(by0 + py, S);
+#ifndef NR_NO_W4
+                        walk_quarter4<FCAP>(s_face, s_q, q, n, lane, xq, yq, near, far, delta, dm, best);
+#else
                         walk_block<FCAP, false, true, uint64_t, true>(s_face, s_q, q, n, lane, xq, yq, near, far, delta,
                                                                       dm, best);
+#endif
                         if (on) {
                             s_dm[pix] = dm;
                             s_best[pix] = best;
@@ -952,11 +1067,12 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
             bits = (wbase + t < g.nwords) ? words[wbase + t] : 0u;
             off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
         }
-        // thread t: pixel (t & 31, t >> 5) of the bin
+        // thread t: pixel (t & 31, t >> 5) of the bin (a quadrant block: of its quadrant only)
         const int fbest = s_best[t];
         {
             const int px = bx0 + (t & 31), py = by0 + (t >> 5);
-            if (px < S && py < S && (ncand > 0 || !fim_sparse)) fimb[(int)__umul24(py, S) + px] = fbest;
+            const bool mine = quad < 0 || (((t >> 4) & 1) == (quad & 1) && ((t >> 9) & 1) == (quad >> 1));
+            if (mine && px < S && py < S && (ncand > 0 || !fim_sparse)) fimb[(int)__umul24(py, S) + px] = fbest;
         }
         if (SHADE && ncand > 0) {
             int* s_fim = reinterpret_cast<int*>(s_raw);
@@ -1100,7 +1216,9 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
         NR_FTSTAMP(4, clock64());
         const int m = t >> 4, n = t & 15;
         const int iy = by0 + 2 * m, ix = bx0 + 2 * n;
-        if ((NTF == 256 || t < 256) && iy + 1 < S && ix + 1 < S) {
+        // (a quadrant block shades its quadrant's 8x8 output pixels)
+        const bool qmine = quad < 0 || ((n >> 3) == (quad & 1) && (m >> 3) == (quad >> 1));
+        if ((NTF == 256 || t < 256) && qmine && iy + 1 < S && ix + 1 < S) {
             int fis[4];
             if (dyn) {
                 const uint32_t q0 = *reinterpret_cast<const uint32_t*>(s_slot + (2 * m) * COARSE + 2 * n);      // d, b

@@ -123,6 +123,10 @@ struct SideStreamTable {
 #define NR_SPLIT_BUCKET 10
 #endif
 constexpr int SPLIT_BUCKET = NR_SPLIT_BUCKET;  // deep bins: >= 512 candidates
+#ifndef NR_QS_CAP
+#define NR_QS_CAP 16
+#endif
+constexpr int QS_CAP = NR_QS_CAP;  // deep bins per list walked by quadrant blocks (a forward that does not split)
 SideStream* side_stream(hipStream_t st) {
     static thread_local SideStreamTable table;
     SideStream* tab = table.tab;
@@ -251,9 +255,20 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     // 256-thread launch then end last; 64: 0.46-0.48 ms; no cap: 0.50 ms; same-box A/Bs, 3 runs each,
     // gpurun_out/e7, e9)
     const int deep_cap = min(Bcap / 8 * g.nbins, deep_slots_per_xcd() * 7 / 8);
+    // a deep-first forward that does not split (e.g. one item, the 50k torus): each list's bins of
+    // >= 512 candidates (up to QS_CAP of them) are walked by four blocks each, one per 16x16 quadrant
+    // (ordered_bin part 3), so the deepest bins, which set the span while most of the chip idles, spread
+    // over four CUs
+#ifndef NR_NO_QS
+    const bool qs = ordered && !side;
+#else
+    const bool qs = false;
+#endif
+    const int lists = B % 8 == 0 ? 8 : 1;
+    const unsigned qs_grid = (unsigned)((long long)g.nbins * B + (qs ? 3 * QS_CAP * lists : 0));
     if (ordered) {
-        nr_launch(k_bin_order, dim3(B % 8 == 0 ? 8 : 1), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,
-                           g.nbins, side ? split_cnt : nullptr, SPLIT_BUCKET, deep_cap);
+        nr_launch(k_bin_order, dim3(lists), dim3(1024), 0, st, bin_part, setup_groups(g), bin_order, B,
+                           g.nbins, (side || qs) ? split_cnt : nullptr, SPLIT_BUCKET, side ? deep_cap : QS_CAP);
         const int e = check_launch("k_bin_order");
         if (e) return e;
     }
@@ -269,7 +284,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         g_last_fwd.store(LaunchRec{ntf, (fuse ? NR_LAUNCH_FUSED_SHADE : 0) |
                                         (fuse && ntf == 256 && (sh.C == MAXC || sh.draw == static_draw(4)) ? NR_LAUNCH_STATIC_CHANNELS : 0) |
                                         (ordered ? NR_LAUNCH_DEEP_FIRST : 0) | (side ? NR_LAUNCH_SPLIT : 0) |
-                                        (ordered && !side && ntf == 1024 ? NR_LAUNCH_DEALT_QUARTERS : 0)});
+                                        (ordered && !side && ntf == 1024 ? NR_LAUNCH_DEALT_QUARTERS : 0) |
+                                        (qs ? NR_LAUNCH_QUADRANTS : 0)});
         if (side) {
             // fork: the side stream waits for the setup and the order; join: the caller's stream waits
             // for the side stream's launch
@@ -277,6 +293,8 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                 return check_launch("hipEventRecord");
             // (a grid of exactly the cap's blocks: every block past a list's deep prefix exits at once, but
             // each still needs a 1024-thread slot to be dispatched in)
+            // (the dealt-quarter variant with its four-faces-per-step walk here instead: car forward 0.427 ->
+            // 0.434 ms, same-box A/B, gpurun_out/w4b: the deep launch takes more of the rest's wave slots)
             nr_launch((k_raster_fwd<1024, true>), dim3(8 * deep_cap), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 1);
             int e = check_launch("k_raster_fwd");
@@ -297,8 +315,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess)
                 return check_launch("hipEventRecord");
         } else if (fuse && ntf == 1024 && ordered)  // deep bins, not split (e.g. one item): dealt quarters
-            nr_launch((k_raster_fwd<1024, true, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
-                               bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
+            nr_launch((k_raster_fwd<1024, true, 0, true>), dim3(qs_grid),
+                      dim3(1024), 0, st, face_records, rs, bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo,
+                      binfg, order, sparse, split_cnt, qs ? 3 : 0);
         else if (fuse && ntf == 1024)
             nr_launch((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
@@ -315,8 +334,9 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             nr_launch((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
                                F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
         else if (ordered)
-            nr_launch((k_raster_fwd<1024, false, 0, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs,
-                               bbox, mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
+            nr_launch((k_raster_fwd<1024, false, 0, true>), dim3(qs_grid),
+                      dim3(1024), 0, st, face_records, rs, bbox, mask, F, g, near, far, delta, fim, sh, nullptr, nullptr,
+                      binfg, order, 0, split_cnt, qs ? 3 : 0);
         else
             nr_launch((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
                                mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);

@@ -218,8 +218,9 @@ def test_cfg5_torus_1024_vs_oracle(oracle_mod, dev):
     hp = nr.RasterizeHyperparam(image_size=512)
     hp.draw_rgb = hp.draw_depth = False
     img2, fim = nrr.rasterize_core(pv, faces, nr.RasterizeParam(), hp, return_face_index=True)
-    # one item: deep bins first, their 4x4 quarters dealt to the waves
+    # one item: deep bins first, each walked by four quadrant blocks, their 4x4 quarters dealt to the waves
     assert _lib.last_launch("k_raster_fwd")[1] & _lib.NR_LAUNCH_DEALT_QUARTERS
+    assert _lib.last_launch("k_raster_fwd")[1] & _lib.NR_LAUNCH_QUADRANTS
     assert torch.equal(img2[:, 0], img.detach())
     img2[:, 0].backward(g.to(dev))
     ref, rfim, rgv, _ = _oracle(oracle_mod, proj.cpu(), f, [0], 512, g[:, None], draw_rgb=False, draw_depth=False)

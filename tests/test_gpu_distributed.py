@@ -108,8 +108,8 @@ def _bench_args(batch):
     return argparse.Namespace(batch=batch, level=4, image_size=256, mode="rgbsd")
 
 
-def _bench_worker(rank, world_size, port, out_dir):
-    """One rank of bench.py's N > 1 step: its own 64 headline items, forward + backward, then the
+def _bench_worker(rank, world_size, port, out_dir, batch=64):
+    """One rank of bench.py's N > 1 step: its own `batch` headline items, forward + backward, then the
     all_reduce of the shared atlas gradient that bench.step issues inside the timed region."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -120,7 +120,7 @@ def _bench_worker(rank, world_size, port, out_dir):
         import bench
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        w = bench.workload(_bench_args(64), rank, dev)
+        w = bench.workload(_bench_args(batch), rank, dev)
         assert w["shared"] == [w["tex"]]
         bench.step(w)
         torch.cuda.synchronize()
@@ -158,6 +158,30 @@ def test_bench_step_allreduce_matches_128_items(tmp_path, dev):
     bench.step(single)
     part = single["tex"].grad.cpu().numpy()
     assert np.abs(part - want_atlas).max() > 1e-2 * np.abs(want_atlas).max()
+
+
+def test_bench_step_allreduce_8_ranks(tmp_path, dev):
+    """cfg4's 8-rank form (batch=512 over 8 GPUs) rehearsed at 8 items per rank: eight gloo
+    ranks on the box's one GPU run bench.py's N > 1 step (bench.workload: rank r renders items
+    8r .. 8r + 7, one shared 288^2 atlas; the step ends with the all_reduce(SUM) of the atlas
+    gradient).  Every rank's atlas gradient equals the gradient of the same 64 items rendered and
+    differentiated in one process, and each rank's projected-vertex gradients equal that process's
+    for its items (within GRAD_TOL).  The RCCL form needs 8 devices (RCCL refuses two ranks on one)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    R, B = 8, 8
+    mp.spawn(_bench_worker, args=(R, _free_port(), str(tmp_path), B), nprocs=R, join=True)
+    got = [np.load(str(tmp_path / ("b%d.npz" % r))) for r in range(R)]
+    w = bench.workload(_bench_args(R * B), 0, dev)
+    w["g"] = torch.as_tensor(np.concatenate([got[r]["g"] for r in range(R)]), device=dev)
+    bench.step(w)
+    want_atlas = w["tex"].grad.cpu().numpy()
+    want_proj = w["proj"].grad.cpu().numpy()
+    assert float(np.abs(want_atlas).sum()) > 0
+    for r in range(R):
+        _close(got[r]["grad_atlas"], want_atlas, "rank %d of 8: all-reduced atlas gradient" % r)
+        _close(got[r]["grad_proj"], want_proj[B * r:B * (r + 1)], "rank %d of 8: projected-vertex gradient" % r)
 
 
 def _rccl_worker(rank, port, out_dir):

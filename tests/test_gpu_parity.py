@@ -356,10 +356,42 @@ def test_face_index_deep_stack_depth_cull(oracle_mod, dev, zlevels):
     hp.draw_rgb = False
     _, fim = nrr.rasterize_core(verts, faces, nr.RasterizeParam(), hp, return_face_index=True)
     ntf, flags = _lib.last_launch("k_raster_fwd")
-    # (not split, B % 8 != 0: the deep bins' quarters dealt to the waves)
+    # (not split, B % 8 != 0: the deep bins' quarters dealt to the waves, each deep bin walked by four
+    # quadrant blocks)
     assert ntf == 1024 and flags & _lib.NR_LAUNCH_DEEP_FIRST and flags & _lib.NR_LAUNCH_DEALT_QUARTERS, (ntf, flags)
+    assert flags & _lib.NR_LAUNCH_QUADRANTS, flags
     assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
     assert (ref[1] >= 0).any() and (ref[1] < 0).any()
+
+
+@pytest.mark.parametrize("B", [1, 8])
+def test_quadrant_split_over_cap_vs_oracle(oracle_mod, dev, B):
+    """More deep bins per deep-first list than the quadrant split takes (NR_QS_CAP = 16): the deepest
+    16 of each list are walked by four quadrant blocks each (ordered_bin part 3), the rest by one
+    block with dealt quarters, and every quarter walk takes four faces per step (walk_quarter4); one
+    list (B = 1, fused silhouettes + depth) and one list per XCD (B = 8, the face-index map alone, a
+    forward that does not split); bit-exact against the brute-force oracle, with depth ties."""
+    r = np.random.RandomState(31 + B)
+    S, F = 192, 16000
+    cx = r.uniform(-0.95, 0.95, size=(B, F, 1))
+    cy = r.uniform(-0.95, 0.95, size=(B, F, 1))
+    x = (cx + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    y = (cy + r.uniform(-0.12, 0.12, size=(B, F, 3))).astype(np.float32)
+    z = r.uniform(0.5, 5.0, size=(B, F, 3)).astype(np.float32)
+    z[:, ::7] = np.float32(2.0)  # every seventh face flat at one depth: ties within depth_min_delta
+    fg = np.stack([x, y, z], -1).astype(np.float32)
+    ref = oracle_mod.face_index_map(torch.as_tensor(fg), S)
+    if B == 1:
+        verts = torch.as_tensor(fg.reshape(B, F * 3, 3), device=dev)
+        faces = torch.arange(F * 3, dtype=torch.int32, device=dev).reshape(F, 3)
+        hp = nr.RasterizeHyperparam(image_size=S, anti_aliasing=False)
+        hp.draw_rgb = False
+        _, fim = nrr.rasterize_core(verts, faces, nr.RasterizeParam(), hp, return_face_index=True)
+    else:
+        fim = nrr.compute_face_index_map(torch.as_tensor(fg, device=dev), nr.RasterizeHyperparam(image_size=S))
+    ntf, flags = _lib.last_launch("k_raster_fwd")
+    assert ntf == 1024 and flags & _lib.NR_LAUNCH_QUADRANTS and not flags & _lib.NR_LAUNCH_SPLIT, (ntf, flags)
+    assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
 
 
 def test_split_forward_capped_vs_oracle(oracle_mod, dev):

@@ -21,8 +21,11 @@ if len(sys.argv) > 2 and sys.argv[1] == "--workload":
     del sys.argv[1:3]
 sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402  (the product's hipcc flags)
-subprocess.check_call(["/opt/rocm/bin/hipcc", *__graft_entry__.hipcc_flags(), "-DNR_FWD_TIMING", "-I" + ROOT + "/include"]
-                      + sys.argv[1:] + [ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib_path])
+if os.environ.get("NR_FTIMING_LIB"):  # a timing build made beforehand (on the CPU host)
+    lib_path = os.environ["NR_FTIMING_LIB"]
+else:
+    subprocess.check_call(["/opt/rocm/bin/hipcc", *__graft_entry__.hipcc_flags(), "-DNR_FWD_TIMING", "-I" + ROOT + "/include"]
+                          + sys.argv[1:] + [ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib_path])
 os.environ["NR_LIB_PATH"] = lib_path
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
@@ -35,6 +38,11 @@ if WORKLOAD == "car":
     import bench_configs  # noqa: E402
     step, _, batch, size = bench_configs.cfg3_step(torch.device("cuda", 0))
     waves = 16  # deep bins: the 1024-thread variant
+elif WORKLOAD == "cfg5":  # the 50k torus, one item at 1024^2 (deep-first, dealt quarters in its deep bins)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs  # noqa: E402
+    step = bench_configs.cfg5_step(torch.device("cuda", 0))[0]
+    batch, size, waves = 1, 512, 16
 elif WORKLOAD == "cfg2":  # the teapot, B = 4 (the 1024-thread variant: small batches)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_configs  # noqa: E402
@@ -68,7 +76,9 @@ if split:
     parts = [("deep launch (1024 threads)", raw[:nbins * bcap * 16 * 10].reshape(nbins * bcap, 16, 10)),
              ("rest launch (256 threads, side stream)", raw[HALF:HALF + nbins * batch * 4 * 10].reshape(nbins * batch, 4, 10))]
 else:
-    parts = [("k_raster_fwd<%d>" % threads, raw[:nbins * batch * waves * 10].reshape(nbins * batch, waves, 10))]
+    # (a deep-first forward that does not split launches 3 x 16 (NR_QS_CAP) quadrant blocks per list beyond its bins)
+    nblk = nbins * batch + (3 * 16 * (8 if batch % 8 == 0 else 1) if flags & _lib.NR_LAUNCH_QUADRANTS else 0)
+    parts = [("k_raster_fwd<%d>" % threads, raw[:nblk * waves * 10].reshape(nblk, waves, 10))]
 # blocks past their launch's part of the deep-first list return before their first stamp
 parts = [(lab, t[t[:, 0, 0] != 0]) for lab, t in parts]
 

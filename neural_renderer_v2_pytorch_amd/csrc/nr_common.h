@@ -152,7 +152,7 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // run_face_index; groups = the setup's face groups of SETUP_FACES)
 size_t ws_bbox_bytes(int B, int F) { return align_up((size_t)B * F * sizeof(int2)); }
 size_t ws_mask_bytes(int B, const Geom& g) { return align_up((size_t)B * g.nbins * g.nwords * 4); }
-inline int setup_groups(const Geom& g) { return (g.nwords + SETUP_FACES / 32 - 1) / (SETUP_FACES / 32); }
+__host__ __device__ inline int setup_groups(const Geom& g) { return (g.nwords + SETUP_FACES / 32 - 1) / (SETUP_FACES / 32); }
 size_t ws_part_bytes(int B, const Geom& g) { return align_up((size_t)B * setup_groups(g) * g.nbins); }
 size_t ws_order_bytes(int B, const Geom& g) { return ws_part_bytes(B, g) + align_up((size_t)B * g.nbins * 4) + 256; }
 

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
                                                     const float* __restrict__ vt, long long vt_bstride, int Vt,
                                                     const int32_t* __restrict__ faces_t, float* __restrict__ face_uv,
                                                     int uv_items, float* __restrict__ fnorm, TexPack pk, ZeroFill zf,
-                                                    uint8_t* __restrict__ bin_part, int xcd_items) {
+                                                    uint8_t* __restrict__ bin_part, int xcd_items, int sparse_groups) {
     __shared__ int2 s_bb[SETUP_FACES];
     // the block's face records, assembled per face and then written out coalesced (a record per lane
     // would store 64-B strided rows); the bin-mask words reuse the space afterwards
@@ -161,6 +161,22 @@ __global__ __launch_bounds__(256) void k_face_setup(const float* __restrict__ ve
             }
         }
         __syncthreads();
+        if (sparse_groups && bin_part) {
+            // (k_bin_order's group lists) a thread per bin writes the group's count and, only where it
+            // has candidates, its words: the forward reads no other piece
+            uint8_t* row = bin_part + ((long long)b * gridDim.x + grp) * nbins;
+            for (int bin = t; bin < nbins; bin += blockDim.x) {
+                const uint32_t* sm = s_mask + bin * (SETUP_FACES / 32);
+                int pc = 0;
+#pragma unroll
+                for (int wi = 0; wi < SETUP_FACES / 32; wi++) pc += __builtin_popcount(sm[wi]);
+                row[bin] = (uint8_t)pc;
+                if (pc)
+                    for (int wi = 0; wi < nw; wi++) mask[((long long)b * nbins + bin) * nwords + w0 + wi] = sm[wi];
+            }
+            zero_fill(zf);
+            return;
+        }
         for (int p = t; p < nbins * nw; p += blockDim.x) {
             const int bin = p / nw, wi = p % nw;
             mask[((long long)b * nbins + bin) * nwords + w0 + wi] = s_mask[bin * (SETUP_FACES / 32) + wi];
@@ -814,7 +830,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                                                   int32_t* __restrict__ fim, Shade sh_in, float* __restrict__ images,
                                                   float* __restrict__ halo, uint8_t* __restrict__ binfg,
                                                   const int* __restrict__ order, int fim_sparse,
-                                                  const int* __restrict__ split, int part) {
+                                                  const int* __restrict__ split, int part,
+                                                  const uint8_t* __restrict__ sg_parts) {
     using C = FwdCfg<NTF>;
     static_assert(!SHADE || ((NTF == 256 || NTF == 1024) && COARSE == 32), "fused shading: threads 0-255 shade a pixel each");
     constexpr int NSUB = C::NSUB, FCAP = C::FCAP, CAND = C::CAND;
@@ -859,8 +876,43 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
 #ifdef NR_FWD_TIMING
     unsigned long long t_stage = 0, t_wait = 0;  // staging rounds; (static blocks) waits after the walks
 #endif
+    // (DQ, sg_parts: sparse groups, a deep-first forward that does not split) the bin's mask words are
+    // read through the list of the face groups with candidates in it, built here from the setup's
+    // per-group counts (thread t: group t) by a block scan, ascending: virtual word v = 6 j + i is word
+    // i of the j-th listed group, so the rounds below expand the same candidates in the same ascending
+    // order while reading only the listed groups' words -- the only ones the setup wrote
+    // (k_face_setup sparse_groups)
+    constexpr int GW = SETUP_FACES / 32;
+    __shared__ uint16_t s_gl[DQ ? NTF : 1];  // (the host takes this path only for <= NTF groups)
+    bool sgm = false;   // (block-uniform)
+    int nv = g.nwords;  // virtual words
+    if (DQ && sg_parts && !known_empty) {
+        const int groups = setup_groups(g);
+        const int c = t < groups ? sg_parts[((long long)b * groups + t) * g.nbins + bin] : 0;
+        int ng;
+        const int o = block_scan<C::NW>(c ? 1 : 0, ng, s_scan);
+        if (c) s_gl[o] = (uint16_t)t;
+        __syncthreads();
+        sgm = true;
+        nv = ng * GW;
+    }
+    // virtual word v's bits, and its word index (wr) in the bin's mask row
+    auto word_at = [&](int v, int& wr) -> uint32_t {
+        if (DQ && sgm) {
+            if (v >= nv) {
+                wr = 0;
+                return 0u;
+            }
+            const int j = v / GW;
+            wr = (int)s_gl[j] * GW + (v - j * GW);
+            return wr < g.nwords ? words[wr] : 0u;
+        }
+        wr = v;
+        return v < g.nwords ? words[v] : 0u;
+    };
     // the first round of mask words and its candidate count
-    const uint32_t bits0 = (!known_empty && t < g.nwords) ? words[t] : 0u;
+    int wr0 = t;
+    const uint32_t bits0 = !known_empty ? word_at(t, wr0) : 0u;
     // (256-thread variant, NTF < nwords <= 2 NTF, e.g. the car's shallow bins in a split forward) the
     // second round of words too, scanned in the same block scan (two 16-bit counts per thread), so a
     // bin whose candidates fit one staging round takes the dealt-block path
@@ -969,9 +1021,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                                               ((quad & 2) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull);
         const bool rows_lo = quad < 0 || !(quad & 2), rows_hi = quad < 0 || (quad & 2);
         uint32_t bits = bits0;
-        int total = total0, off = off0;
+        int total = total0, off = off0, w = wr0;
         for (int wbase = 0;;) {
-            const int w = wbase + t;
             ncand += total;
             for (int cbase = 0; cbase < total; cbase += CAND) {
                 int r = off;
@@ -1063,8 +1114,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                 }
             }
             wbase += NTF;
-            if (wbase >= g.nwords) break;
-            bits = (wbase + t < g.nwords) ? words[wbase + t] : 0u;
+            if (wbase >= nv) break;
+            bits = word_at(wbase + t, w);
             off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
         }
         // thread t: pixel (t & 31, t >> 5) of the bin (a quadrant block: of its quadrant only)
@@ -1097,9 +1148,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
             best[k] = -1;
         }
         uint32_t bits = bits0;
-        int total = total0, off = off0;
+        int total = total0, off = off0, w = wr0;
         for (int wbase = 0;;) {
-            const int w = wbase + t;
             ncand += total;
             for (int cbase = 0; cbase < total; cbase += CAND) {
                 // expand my word's set bits into the ordered candidate list
@@ -1148,8 +1198,8 @@ __global__ __launch_bounds__(NTF) __attribute__((amdgpu_waves_per_eu(FWD_WPE, 8)
                 }
             }
             wbase += NTF;
-            if (wbase >= g.nwords) break;
-            bits = (wbase + t < g.nwords) ? words[wbase + t] : 0u;
+            if (wbase >= nv) break;
+            bits = word_at(wbase + t, w);
             off = block_scan<C::NW>(__builtin_popcount(bits), total, s_scan);
         }
 #pragma unroll

@@ -202,6 +202,24 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
     if (F == 0 && zf.p && hipMemsetAsync(zf.p, 0, (size_t)zf.n16 * 16, st) != hipSuccess)
         return check_launch("hipMemsetAsync");
 
+    // k_shade's work fused into the forward's 256-thread variant (anti-aliasing, no lights or
+    // backgrounds): the face-index map is not read back, and there is one launch fewer
+    const Shade sh = ra ? make_shade(ra) : Shade{};
+    // the deep-bin / small-grid 1024-thread variant shades too (its threads 0-255)
+    const bool fuse = ra && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
+    // the split forward (below) when the batch is deep-first, fused and B % 8 == 0; otherwise a
+    // deep-first forward reads its bins' mask words through sparse groups: the setup writes only the
+    // (group, bin) pieces with candidates, and each forward block lists its bin's groups from the
+    // setup's counts (for the 50k torus at 1024^2: 1024 bins x 1563 words of dense masks for ~10^4
+    // non-empty pieces).  A split that finds no side stream falls back to the dense reads (the setup
+    // wrote every piece)
+    const int Bcap = B % 8 == 0 ? max(8, (B / 4 + 7) / 8 * 8) : 0;
+    const bool want_split = ordered && fuse && B % 8 == 0 && Bcap <= B;
+#ifndef NR_NO_SPARSE_GROUPS
+    const bool sg = ordered && !want_split && setup_groups(g) <= 1024;
+#else
+    const bool sg = false;
+#endif
     if (F > 0) {
         dim3 grid((F + SETUP_FACES - 1) / SETUP_FACES, B);
         const bool rgb = ra && (ra->draw_flags & NR_DRAW_RGB);
@@ -215,11 +233,11 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
                                rgb ? ra->vertices_textures : nullptr, rgb ? ra->vt_batch_stride : 0,
                                rgb ? ra->num_vertices_textures : 0, rgb ? ra->faces_textures : nullptr,
                                rgb ? ra->face_uv : nullptr, uv_items, lit ? ra->face_normals : nullptr, pk, zf,
-                               ordered ? bin_part : nullptr, B % 8 == 0);
+                               ordered ? bin_part : nullptr, B % 8 == 0, sg ? 1 : 0);
         else
             nr_launch(k_face_setup<false>, grid, dim3(256), lds, st, nullptr, nullptr, face_records, V, F, S,
                                draw_backside, bbox, mask, g.nbx, g.nbins, g.nwords, nullptr, 0, 0, nullptr, nullptr, 0,
-                               nullptr, pk, zf, ordered ? bin_part : nullptr, B % 8 == 0);
+                               nullptr, pk, zf, ordered ? bin_part : nullptr, B % 8 == 0, sg ? 1 : 0);
         int e = check_launch("k_face_setup");
         if (e) return e;
         if (lit && V > 0) {
@@ -230,21 +248,15 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             if (e) return e;
         }
     }
-    // k_shade's work fused into the forward's 256-thread variant (anti-aliasing, no lights or
-    // backgrounds): the face-index map is not read back, and there is one launch fewer
-    const Shade sh = ra ? make_shade(ra) : Shade{};
-    // the deep-bin / small-grid 1024-thread variant shades too (its threads 0-255)
-    const bool fuse = ra && ra->anti_aliasing && sh.nl == 0 && !sh.bg && vertices;
     // split forward (deep-bin batches of B % 8 == 0 items, e.g. the car): the bins with >= 2^(SPLIT_BUCKET
     // - 1) candidates (a prefix of each deep-first list, at most Bcap / 8 * nbins of them) in the
     // 1024-thread variant on the caller's stream, the rest in the 256-thread variant on a side stream at
     // the same time: a shallow bin's 16 waves in the 1024-thread variant mostly wait for their block's
     // slowest wave, where the 256-thread variant deals its 16 8x8 blocks to 4 waves
-    const int Bcap = B % 8 == 0 ? max(8, (B / 4 + 7) / 8 * 8) : 0;
     int* split_cnt = (int*)((char*)bin_order + align_up((size_t)B * g.nbins * 4));
     SideStream* side = nullptr;
 #ifndef NR_NO_SPLIT
-    if (ordered && fuse && B % 8 == 0 && Bcap <= B) side = side_stream(st);
+    if (want_split) side = side_stream(st);
 #endif
     // the deep launch takes at most 7/8 of one XCD's slots for 1024-thread blocks per list (two per CU,
     // by their waves and LDS), so every deep bin is dispatched at once: a deep block waiting for a slot
@@ -296,20 +308,20 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
             // (the dealt-quarter variant with its four-faces-per-step walk here instead: car forward 0.427 ->
             // 0.434 ms, same-box A/B, gpurun_out/w4b: the deep launch takes more of the rest's wave slots)
             nr_launch((k_raster_fwd<1024, true>), dim3(8 * deep_cap), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 1);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 1, nullptr);
             int e = check_launch("k_raster_fwd");
             if (e) return e;
             if (sh.C == MAXC)
                 nr_launch((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
                                    bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
-                                   split_cnt, 2);
+                                   split_cnt, 2, nullptr);
             else if (sh.draw == static_draw(4))  // rgba (the car): compile-time channels
                 nr_launch((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs,
                                    bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse,
-                                   split_cnt, 2);
+                                   split_cnt, 2, nullptr);
             else
                 nr_launch((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, side->s, face_records, rs, bbox,
-                                   mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 2);
+                                   mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, split_cnt, 2, nullptr);
             e = check_launch("k_raster_fwd");
             if (e) return e;
             if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess)
@@ -317,29 +329,29 @@ static int run_face_index(const float* vertices, const int32_t* faces_idx, float
         } else if (fuse && ntf == 1024 && ordered)  // deep bins, not split (e.g. one item): dealt quarters
             nr_launch((k_raster_fwd<1024, true, 0, true>), dim3(qs_grid),
                       dim3(1024), 0, st, face_records, rs, bbox, mask, F, g, near, far, delta, fim, sh, images, ra->halo,
-                      binfg, order, sparse, split_cnt, qs ? 3 : 0);
+                      binfg, order, sparse, split_cnt, qs ? 3 : 0, sg ? bin_part : nullptr);
         else if (fuse && ntf == 1024)
             nr_launch((k_raster_fwd<1024, true>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0, nullptr);
         else if (fuse && sh.C == MAXC)  // rgb + sil + depth: compile-time channels
             nr_launch((k_raster_fwd<256, true, MAXC>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0, nullptr);
         else if (fuse && sh.draw == static_draw(4))  // rgba: compile-time channels
             nr_launch((k_raster_fwd<256, true, 4>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
+                               mask, F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0, nullptr);
         else if (fuse)
             nr_launch((k_raster_fwd<256, true>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0);
+                               F, g, near, far, delta, fim, sh, images, ra->halo, binfg, order, sparse, nullptr, 0, nullptr);
         else if (ntf == 256)
             nr_launch((k_raster_fwd<256, false>), dim3(g.nbins, B), dim3(256), 0, st, face_records, rs, bbox, mask,
-                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
+                               F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0, nullptr);
         else if (ordered)
             nr_launch((k_raster_fwd<1024, false, 0, true>), dim3(qs_grid),
                       dim3(1024), 0, st, face_records, rs, bbox, mask, F, g, near, far, delta, fim, sh, nullptr, nullptr,
-                      binfg, order, 0, split_cnt, qs ? 3 : 0);
+                      binfg, order, 0, split_cnt, qs ? 3 : 0, sg ? bin_part : nullptr);
         else
             nr_launch((k_raster_fwd<1024, false>), dim3(g.nbins, B), dim3(1024), 0, st, face_records, rs, bbox,
-                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0);
+                               mask, F, g, near, far, delta, fim, sh, nullptr, nullptr, binfg, order, 0, nullptr, 0, nullptr);
     }
     int e = check_launch("k_raster_fwd");
     if (e || !ra || fuse) return e;

@@ -253,6 +253,7 @@ __device__ __forceinline__ int count_bucket(int c) { return c <= 0 ? 0 : min(ORD
 // the chunk's lanes of the same bucket.  Stable: screen order (and so neighbouring bins, which share
 // face records in L2) within a bucket -- an unstable order cost the car's forward ~6 us.
 constexpr int ORDER_MAX_ENTRIES = 64 * 256;
+constexpr int ORDER_SLICED_MAX = 2048;  // k_bin_order: lists of up to 2 x 1024 entries are summed in slices
 // (ORDER_EMPTY, the entry flag of a bin without candidates, is in nr_common.h with ordered_bin)
 // split (optional): per list, the length of its prefix of bins with >= 2^(split_bucket - 1) candidate
 // faces, at most cap (the deep launch of a split forward, run_face_index)
@@ -276,7 +277,37 @@ __global__ __launch_bounds__(1024) void k_bin_order(const uint8_t* __restrict__ 
     };
     // each entry's candidate count, the face groups' counts summed, as its bucket: four consecutive
     // bins of an item per thread and 32-bit loads when the bins come in fours (a multiple of 4 per item)
-    if (nbins % 4 == 0) {
+    // (fewer quads than threads, e.g. one item's bins: S threads per quad share its groups, the loads of
+    // a quad's S slices in flight at once, summed in LDS -- the torus's one list of 256 quads over 261
+    // groups took 20.6 us a thread per quad)
+    const int quads = nbins % 4 == 0 ? n / 4 : 0;
+    int S = 1;
+    while (quads > 0 && S < 8 && 2 * S * quads <= (int)blockDim.x) S *= 2;
+    if (S > 1) {
+        __shared__ int s_cnt[ORDER_SLICED_MAX];
+        for (int k = threadIdx.x; k < n; k += blockDim.x) s_cnt[k] = 0;
+        __syncthreads();
+        const int q = threadIdx.x % quads, sl = threadIdx.x / quads;
+        if (sl < S) {
+            const int k = 4 * q, e = entry(k), b = e / nbins, bin = e - b * nbins;
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(parts + (long long)b * groups * nbins + bin);
+            int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll 8
+            for (int gr = sl; gr < groups; gr += S) {
+                const uint32_t v = p[(long long)gr * (nbins / 4)];
+                c0 += v & 0xffu;
+                c1 += (v >> 8) & 0xffu;
+                c2 += (v >> 16) & 0xffu;
+                c3 += v >> 24;
+            }
+            atomicAdd(&s_cnt[k], c0);
+            atomicAdd(&s_cnt[k + 1], c1);
+            atomicAdd(&s_cnt[k + 2], c2);
+            atomicAdd(&s_cnt[k + 3], c3);
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < n; k += blockDim.x) s_bk[k] = (uint8_t)count_bucket(s_cnt[k]);
+    } else if (nbins % 4 == 0) {
         for (int q = threadIdx.x; q < n / 4; q += blockDim.x) {
             const int k = 4 * q, e = entry(k), b = e / nbins, bin = e - b * nbins;
             const uint32_t* p = reinterpret_cast<const uint32_t*>(parts + (long long)b * groups * nbins + bin);

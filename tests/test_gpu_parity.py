@@ -394,6 +394,28 @@ def test_quadrant_split_over_cap_vs_oracle(oracle_mod, dev, B):
     assert np.array_equal(fim.cpu().numpy(), ref), int((fim.cpu().numpy() != ref).sum())
 
 
+def test_sparse_groups_cap_dense_fallback_vs_oracle(oracle_mod, dev):
+    """A deep-first forward that does not split with more face groups than the sparse-group path takes
+    (200k faces: 1042 groups of 192 > 1024, one forward thread per group): the setup writes the dense
+    masks and the forward reads them whole, with the quadrant blocks and the four-face quarter walk;
+    bit-exact against the brute-force oracle (and the same faces at 160k, 834 groups, through the sparse
+    groups)."""
+    r = np.random.RandomState(41)
+    S = 64
+    for F in (200000, 160000):
+        cx = r.uniform(-0.9, 0.9, size=(1, F, 1))
+        cy = r.uniform(-0.9, 0.9, size=(1, F, 1))
+        x = (cx + r.uniform(-0.05, 0.05, size=(1, F, 3))).astype(np.float32)
+        y = (cy + r.uniform(-0.05, 0.05, size=(1, F, 3))).astype(np.float32)
+        z = r.uniform(0.5, 5.0, size=(1, F, 3)).astype(np.float32)
+        fg = np.stack([x, y, z], -1).astype(np.float32)
+        ref = oracle_mod.face_index_map(torch.as_tensor(fg), S)
+        fim = nrr.compute_face_index_map(torch.as_tensor(fg, device=dev), nr.RasterizeHyperparam(image_size=S))
+        ntf, flags = _lib.last_launch("k_raster_fwd")
+        assert ntf == 1024 and flags & _lib.NR_LAUNCH_QUADRANTS, (F, ntf, flags)
+        assert np.array_equal(fim.cpu().numpy(), ref), (F, int((fim.cpu().numpy() != ref).sum()))
+
+
 def test_split_forward_capped_vs_oracle(oracle_mod, dev):
     """The split forward (fused, anti-aliased, B % 8 == 0): every bin holds 1000+ candidates, so each
     deep-first list's deep prefix is capped (a quarter of the items' bins may go to the 1024-thread

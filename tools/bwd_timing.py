@@ -2,6 +2,7 @@
 cfg3) (timing build, NR_BWD_TIMING).
 
 usage (GPU box): python tools/bwd_timing.py [--workload car] [extra -D flags...]
+(NR_BTIMING_LIB=<path>: a timing build made beforehand, -DNR_BWD_TIMING, instead of building here)
 Builds the library with -DNR_BWD_TIMING into /tmp, runs bench.py's headline step through it, reads
 the per-wave shader-clock stamps of the last backward (nr_debug_bwd_timing) and prints the mean and
 percentiles of each phase: step 1 (recompute + staging of I and G), barrier 1, stencil, barrier 2,
@@ -21,8 +22,11 @@ if len(sys.argv) > 2 and sys.argv[1] == "--workload":
     del sys.argv[1:3]
 sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402  (the product's hipcc flags)
-subprocess.check_call(["/opt/rocm/bin/hipcc", *__graft_entry__.hipcc_flags(), "-DNR_BWD_TIMING", "-I" + ROOT + "/include"]
-                      + sys.argv[1:] + [ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib_path])
+if os.environ.get("NR_BTIMING_LIB"):  # a timing build made beforehand (on the CPU host)
+    lib_path = os.environ["NR_BTIMING_LIB"]
+else:
+    subprocess.check_call(["/opt/rocm/bin/hipcc", *__graft_entry__.hipcc_flags(), "-DNR_BWD_TIMING", "-I" + ROOT + "/include"]
+                          + sys.argv[1:] + [ROOT + "/neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip", "-o", lib_path])
 os.environ["NR_LIB_PATH"] = lib_path
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402

@@ -1,6 +1,7 @@
-# usage: VARIANTS="base lib:abl/libnr_old.so NR_FWD_TIMING A=1,@ENV=2" bash tools/ablate.sh <tag>
+# usage: VARIANTS="base lib:abl/libnr_old.so NR_FWD_TIMING A=1,@ENV=2 M:--misched=gcn-max-ilp" bash tools/ablate.sh <tag>
 # builds one library per variant (comma-separated -D defines; "base" = none; a token @VAR=value is an
-# environment setting of that variant's runs instead) and benches each;
+# environment setting of that variant's runs instead, M:<opt> an `-mllvm <opt>` code-generation option)
+# and benches each;
 # CONFIGS=cfg2,cfg3,cfg5 also times those configs (tools/bench_configs.py); NOHEAD=1 skips the headline.
 set -o pipefail
 # the product's hipcc flags (__graft_entry__.HIPCC_FLAGS without -I); HIPFLAGS overrides them
@@ -17,7 +18,7 @@ for V in $VARIANTS; do
   V0=${V%%,*}
   if [ "${V0#lib:}" != "$V0" ]; then cp "${V0#lib:}" $OUT/lib/libnr_$i.so || exit 1; continue; fi
   DEFS=""
-  if [ "$V" != base ]; then for d in ${V//,/ }; do case $d in @*) ;; base) ;; lib:*) ;; *) DEFS="$DEFS -D$d";; esac; done; fi
+  if [ "$V" != base ]; then for d in ${V//,/ }; do case $d in @*) ;; base) ;; lib:*) ;; M:*) DEFS="$DEFS -mllvm ${d#M:}";; *) DEFS="$DEFS -D$d";; esac; done; fi
   /opt/rocm/bin/hipcc $HIPFLAGS \
   -Iinclude $DEFS neural_renderer_v2_pytorch_amd/csrc/nr_raster.hip -o $OUT/lib/libnr_$i.so || exit 1
 done

@@ -1,4 +1,4 @@
-"""Batch sharding across ranks on CPU with gloo, world_size 2.
+"""Batch sharding across ranks on CPU with gloo, world_size 2 and 8.
 
 Each rank renders its shard of the batch (here with the CPU oracle standing in for the GPU, which
 the sharding logic does not depend on), the shards are assembled with gather_images, and the
@@ -92,6 +92,26 @@ def test_gloo_world2_matches_full_batch(tmp_path, oracle_mod, batch):
     images = _render(oracle_mod, base, faces, shifts)
     _loss(images, shifts).backward()
     for r in range(2):
+        got = np.load(str(tmp_path / ("r%d.npz" % r)))
+        assert np.array_equal(got["images"], images.detach().numpy())
+        assert np.array_equal(got["images_known"], images.detach().numpy())
+        np.testing.assert_allclose(got["grad"], base.grad.numpy(), rtol=1e-5, atol=1e-6)
+    assert float(base.grad.abs().sum()) > 0
+
+
+@pytest.mark.parametrize("batch", [16, 13])
+def test_gloo_world8_matches_full_batch(tmp_path, oracle_mod, batch):
+    """cfg4's form (one rank per GPU of an 8-GPU node) rehearsed with eight gloo
+    ranks: each renders its shard (2 items each, or 1-2 for an uneven 13), the shared mesh's
+    gradient is summed over the eight ranks and every rank assembles the whole batch in rank order;
+    both equal the single-process full batch."""
+    ws = 8
+    mp.spawn(_worker, args=(ws, _free_port(), batch, str(tmp_path)), nprocs=ws, join=True)
+    base, faces, shifts = _scene(batch)
+    base.requires_grad_(True)
+    images = _render(oracle_mod, base, faces, shifts)
+    _loss(images, shifts).backward()
+    for r in range(ws):
         got = np.load(str(tmp_path / ("r%d.npz" % r)))
         assert np.array_equal(got["images"], images.detach().numpy())
         assert np.array_equal(got["images_known"], images.detach().numpy())
